@@ -1,0 +1,165 @@
+/*
+ * riptide_amd.h -- C ABI of the MI355X-native FFA periodogram engine.
+ *
+ * This is the drop-in boundary for riptide's native module `riptide.libcpp`
+ * (pybind11, /root/reference/riptide/cpp/python_bindings.cpp:213-267).  Each
+ * host-buffer entry point below replaces one binding of that module, with the
+ * same argument meaning, output shape/dtype and error text; the Python shim
+ * riptide_amd/libcpp.py (or the ctypes stub in INTEGRATION.md) maps them onto
+ * the reference's function names.  All compute runs in HIP kernels on the
+ * current device; there is no CPU compute path.
+ *
+ * Conventions
+ *  - Return value: RT_OK (0) on success; RT_EINVAL for the cases where the
+ *    reference throws std::invalid_argument / std::domain_error (Python
+ *    ValueError); RT_EHIP for a HIP runtime failure; RT_EINTERNAL otherwise.
+ *    rt_last_error() returns the message of the calling thread's last failure
+ *    (the reference's exception text for RT_EINVAL).
+ *  - "host" pointers are ordinary CPU memory (numpy buffers); "device"
+ *    pointers are HIP device memory; `stream` is a hipStream_t (NULL = the
+ *    library's own stream).  Host-buffer calls are synchronous.
+ *  - Widths are uint64 (size_t in the reference).
+ */
+#ifndef RIPTIDE_AMD_H
+#define RIPTIDE_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_OK 0
+#define RT_EINVAL 1
+#define RT_EHIP 2
+#define RT_EINTERNAL 3
+
+const char* rt_last_error(void);
+/* Version string of the engine and the gfx target it was built for. */
+const char* rt_version(void);
+/* Select the HIP device used by subsequent host-buffer calls of this thread. */
+int rt_set_device(int device);
+
+/* ---------------- host-buffer drop-ins for riptide.libcpp ----------------- */
+
+/* python_bindings.cpp:32-40  rollback(x, shift): out = roll(x, -shift) */
+int rt_rollback(const float* x, size_t size, size_t shift, float* out);
+
+/* python_bindings.cpp:43-58  fused_rollback_add(x, y, shift): out = x + roll(y, -shift) */
+int rt_fused_rollback_add(const float* x, const float* y, size_t size, size_t shift, float* out);
+
+/* python_bindings.cpp:61-69  circular_prefix_sum(x, nsum): out has nsum elements */
+int rt_circular_prefix_sum(const float* x, size_t size, size_t nsum, float* out);
+
+/* python_bindings.cpp:72-84  ffa2(data[rows, cols]) -> out[rows, cols] */
+int rt_ffa2(const float* in, size_t rows, size_t cols, float* out);
+
+/* python_bindings.cpp:87-106  benchmark_ffa2(rows, cols, loops) -> seconds per loop
+ * (device-resident zero input, HIP-event timed) */
+int rt_benchmark_ffa2(size_t rows, size_t cols, size_t loops, double* seconds);
+
+/* python_bindings.cpp:109-126  snr1(data[size], widths, stdnoise) -> out[num_widths] */
+int rt_snr1(const float* x, size_t size, const uint64_t* widths, size_t num_widths, float stdnoise, float* out);
+
+/* python_bindings.cpp:129-148  snr2(data[rows, cols], widths, stdnoise) -> out[rows, num_widths] */
+int rt_snr2(const float* x, size_t rows, size_t cols, const uint64_t* widths, size_t num_widths,
+            float stdnoise, float* out);
+
+/* downsample.hpp:21-24  floor(size / f) */
+size_t rt_downsampled_size(size_t size, double f);
+
+/* python_bindings.cpp:151-165  downsample(data, factor) -> out[rt_downsampled_size(size, factor)] */
+int rt_downsample(const float* x, size_t size, double factor, float* out);
+
+/* periodogram.hpp:63-109  number of trial periods (validates arguments) */
+int rt_periodogram_length(size_t size, double tsamp, double period_min, double period_max,
+                          size_t bins_min, size_t bins_max, size_t* length);
+
+/* python_bindings.cpp:168-197  periodogram(data, tsamp, widths, period_min, period_max,
+ * bins_min, bins_max) -> periods[L] (f64), foldbins[L] (u32), snrs[L, num_widths] (f32) */
+int rt_periodogram(const float* data, size_t size, double tsamp, const uint64_t* widths, size_t num_widths,
+                   double period_min, double period_max, size_t bins_min, size_t bins_max,
+                   double* periods, uint32_t* foldbins, float* snrs);
+
+/* python_bindings.cpp:200-210  running_median(data, width) -> out[size] */
+int rt_running_median(const float* x, size_t size, size_t width, float* out);
+
+/* running_medians.py:49-83 fast_running_median(data, width_samples, min_points) for a
+ * scrunch factor > 1: float32 block means, exact running median of width
+ * min_points, np.interp back to full resolution -> out[size] (float64).  A
+ * scrunch factor of 1 is rt_running_median (the reference returns float32 then). */
+int rt_fast_running_median(const float* x, size_t size, size_t width_samples, size_t min_points, double* out);
+
+/* time_series.py:93-122 + :66-90 (TimeSeries.deredden(width_samples, minpts) then
+ * .normalise()), one series; either stage may be skipped. width_samples is
+ * int(round(rmed_width / tsamp)) computed by the caller (Python round). */
+int rt_deredden_normalise(const float* x, size_t size, size_t width_samples, size_t min_points,
+                          int deredden, int normalise, float* out);
+
+/* periodogram.hpp:260-264  trial-period grid only (host computation, no device) */
+int rt_periodogram_grid(size_t size, double tsamp, double period_min, double period_max, size_t bins_min,
+                        size_t bins_max, double* periods, uint32_t* foldbins);
+
+/* Host-only: build the FFA pass schedule for a periodogram and verify its
+ * invariants (tiles inside nodes, LDS budget, final pass covers every row). */
+int rt_schedule_check(size_t size, double tsamp, size_t num_widths, double period_min, double period_max,
+                      size_t bins_min, size_t bins_max, uint64_t* transforms, uint64_t* items,
+                      uint64_t* launches, double* alg_bytes_per_trial, double* moved_bytes_per_trial,
+                      uint64_t* cells_per_trial);
+
+/* ------------------ device-resident batched hot path ---------------------- */
+
+typedef struct rt_plan rt_plan;
+
+/* Build the periodogram plan (ladder, grid, pass schedule) once per
+ * (size, tsamp, widths, period range, bins range).  Validates like
+ * periodogram.hpp:25-40 and snr.hpp:21-31 (widths < bins_min). */
+int rt_plan_create(size_t size, double tsamp, const uint64_t* widths, size_t num_widths,
+                   double period_min, double period_max, size_t bins_min, size_t bins_max,
+                   rt_plan** plan);
+void rt_plan_destroy(rt_plan* plan);
+/* L (number of trial periods) and W (number of widths). */
+int rt_plan_shape(const rt_plan* plan, size_t* length, size_t* num_widths);
+/* Host copy of the trial-period grid (bit-exact with the reference). */
+int rt_plan_grid(const rt_plan* plan, double* periods, uint32_t* foldbins);
+/* Device workspace bytes needed to process `batch` trials per call. */
+int rt_plan_workspace_bytes(const rt_plan* plan, size_t batch, size_t* bytes);
+
+/* Periodogram S/N of `batch` series resident in device memory.
+ *   d_data  : batch x size floats, series b at d_data + b * data_stride
+ *   d_snrs  : batch x (L * W) floats, trial b at d_snrs + b * snr_stride
+ * The series must already be dereddened/normalised as the caller wants
+ * (rt_deredden_normalise_device).  Stream-ordered, no host synchronisation. */
+int rt_periodogram_device(const rt_plan* plan, const float* d_data, size_t batch, size_t data_stride,
+                          float* d_snrs, size_t snr_stride, void* d_workspace, size_t workspace_bytes,
+                          void* stream);
+
+/* Device workspace bytes for rt_deredden_normalise_device. */
+int rt_deredden_workspace_bytes(size_t size, size_t width_samples, size_t min_points, size_t batch,
+                                size_t* bytes);
+/* Batched dereddening + normalisation in device memory (d_out may equal d_in
+ * only when deredden == 0). */
+int rt_deredden_normalise_device(const float* d_in, size_t size, size_t batch, size_t in_stride,
+                                 size_t width_samples, size_t min_points, int deredden, int normalise,
+                                 float* d_out, size_t out_stride, void* d_workspace, size_t workspace_bytes,
+                                 void* stream);
+
+/* ----------------------------- profiling ---------------------------------- */
+/* When enabled, rt_periodogram_device records HIP events around every cone
+ * (FFA pass) launch and accumulates their time and algorithmic bytes
+ * (4mp read + 4mp or 4*rows_eval*W written per pass). */
+int rt_profile_enable(int on);
+/* kind: 0 = FFA cone passes, 1 = downsample ladder.  Synchronises the events. */
+int rt_profile_read(int kind, double* milliseconds, double* alg_bytes, double* moved_bytes, uint64_t* launches);
+int rt_profile_reset(void);
+
+/* Plan statistics: transforms, work items, passes, cone launches per trial. */
+int rt_plan_stats(const rt_plan* plan, uint64_t* transforms, uint64_t* items, uint64_t* launches,
+                  double* alg_bytes_per_trial, double* moved_bytes_per_trial, uint64_t* cells_per_trial);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RIPTIDE_AMD_H */

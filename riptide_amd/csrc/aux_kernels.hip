@@ -1,0 +1,487 @@
+// Auxiliary HIP kernels of the hot path: standalone boxcar S/N (snr1/snr2
+// entry points), exact running median, dereddening (scrunch -> running median
+// -> linear interpolation -> subtract) and fp64 normalisation, plus the small
+// kernel-API helpers (rollback, fused_rollback_add, circular_prefix_sum).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace rt {
+
+__device__ __forceinline__ double wave_scan_d(double v, int lane)
+{
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double y = __shfl_up(v, o, 64);
+        if (lane >= o) v += y;
+    }
+    return v;
+}
+
+__device__ __forceinline__ float wave_max_f(float v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// Boxcar S/N over rows of a block (snr.hpp:37-65).  Two launches: (1) fp64
+// circular prefix sums of each row into `cps` + the row sum, (2) per-width
+// maximum of c[i+w] - c[i].  One wave per row.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void snr_prefix_kernel(const float* __restrict__ x, uint64_t rows,
+                                                         uint32_t cols, float* __restrict__ cps,
+                                                         float* __restrict__ sums)
+{
+    const int lane = threadIdx.x & 63;
+    const uint64_t r = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    const float* xr = x + r * cols;
+    float* cr = cps + r * cols;
+    const uint32_t c = (cols + 63) / 64;
+    const uint32_t j0 = min(lane * c, cols), j1 = min(j0 + c, cols);
+    double part = 0.0;
+    for (uint32_t j = j0; j < j1; ++j) part += (double)xr[j];
+    const double incl = wave_scan_d(part, lane);
+    double acc = __shfl_up(incl, 1, 64);
+    if (lane == 0) acc = 0.0;
+    for (uint32_t j = j0; j < j1; ++j) {
+        acc += (double)xr[j];
+        cr[j] = (float)acc;
+    }
+    const float total = __shfl((float)acc, (int)((cols - 1) / c), 64);
+    if (lane == 0) sums[r] = total;
+}
+
+__global__ __launch_bounds__(256) void snr_width_kernel(const float* __restrict__ cps, const float* __restrict__ sums,
+                                                        uint64_t rows, uint32_t cols,
+                                                        const uint32_t* __restrict__ widths, uint32_t nw,
+                                                        float stdnoise, float* __restrict__ out)
+{
+    const int lane = threadIdx.x & 63;
+    const uint64_t r = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    const float* cr = cps + r * cols;
+    const float sum = sums[r];
+    const uint32_t c = (cols + 63) / 64;
+    const uint32_t j0 = min(lane * c, cols), j1 = min(j0 + c, cols);
+    for (uint32_t iw = 0; iw < nw; ++iw) {
+        const uint32_t w = widths[iw];
+        float dmax = -INFINITY;
+        for (uint32_t i = j0; i < j1; ++i) {
+            const uint32_t k = i + w;
+            const float ck = k < cols ? cr[k] : __fadd_rn(cr[k - cols], sum);
+            dmax = fmaxf(dmax, __fsub_rn(ck, cr[i]));
+        }
+        dmax = wave_max_f(dmax);
+        if (lane == 0) {
+            const float h = sqrtf((float)(cols - w) / (float)((uint64_t)cols * w));
+            const float b = (float)w / (float)(cols - w) * h;
+            out[r * nw + iw] = ((h + b) * dmax - b * sum) / stdnoise;
+        }
+    }
+}
+
+hipError_t launch_snr_rows(const float* x, uint64_t rows, uint32_t cols, const uint32_t* d_widths,
+                           uint32_t nw, float stdnoise, float* cps_scratch, float* out, hipStream_t s)
+{
+    if (!rows) return hipSuccess;
+    const uint32_t blocks = (uint32_t)((rows + 3) / 4);
+    float* sums = cps_scratch + rows * cols;
+    hipLaunchKernelGGL(snr_prefix_kernel, dim3(blocks), dim3(256), 0, s, x, rows, cols, cps_scratch, sums);
+    hipLaunchKernelGGL(snr_width_kernel, dim3(blocks), dim3(256), 0, s, cps_scratch, sums, rows, cols,
+                       d_widths, nw, stdnoise, out);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Running median (running_median.hpp:100-132): out[i] = the (w/2)-th order
+// statistic of x[clamp(i - w/2 + j, 0, n-1)], j in [0, w).  Exact: the result
+// is one of the window's values, as with the reference's quickselect.
+// ---------------------------------------------------------------------------
+constexpr int kRmedTile = 256;
+constexpr int kRmedSmallMax = 255;
+
+// Small windows: the block stages its span in LDS; one thread per output
+// counts, for each candidate, how many window values are < and <= it.
+__global__ __launch_bounds__(kRmedTile) void rmed_small_kernel(const float* __restrict__ x, uint64_t n, int width,
+                                                               float* __restrict__ out, uint64_t x_stride,
+                                                               uint64_t out_stride)
+{
+    __shared__ float span[kRmedTile + kRmedSmallMax];
+    x += (uint64_t)blockIdx.y * x_stride;
+    out += (uint64_t)blockIdx.y * out_stride;
+    const int half = width / 2;
+    const int64_t i0 = (int64_t)blockIdx.x * kRmedTile;
+    for (int k = threadIdx.x; k < kRmedTile + width - 1; k += kRmedTile) {
+        int64_t idx = i0 - half + k;
+        idx = idx < 0 ? 0 : (idx >= (int64_t)n ? (int64_t)n - 1 : idx);
+        span[k] = x[idx];
+    }
+    __syncthreads();
+    const int64_t i = i0 + threadIdx.x;
+    if (i >= (int64_t)n) return;
+    const float* win = span + threadIdx.x;
+    float res = win[half];
+    for (int j = 0; j < width; ++j) {
+        const float v = win[j];
+        int less = 0, leq = 0;
+        for (int k = 0; k < width; ++k) {
+            const float u = win[k];
+            less += u < v;
+            leq += u <= v;
+        }
+        if (less <= half && half < leq) { res = v; break; }
+    }
+    out[i] = res;
+}
+
+__device__ __forceinline__ uint32_t float_key(float v)
+{
+    const uint32_t b = __float_as_uint(v);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+__device__ __forceinline__ float key_float(uint32_t k)
+{
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+
+// Large windows: one block per output, radix select on order-preserving keys.
+__global__ __launch_bounds__(256) void rmed_large_kernel(const float* __restrict__ x, uint64_t n, int width,
+                                                         float* __restrict__ out, uint64_t x_stride,
+                                                         uint64_t out_stride)
+{
+    __shared__ int wsum[4];
+    x += (uint64_t)blockIdx.y * x_stride;
+    out += (uint64_t)blockIdx.y * out_stride;
+    const int64_t i = blockIdx.x;
+    const int half = width / 2;
+    uint32_t prefix = 0, mask = 0;
+    int k = half;
+    for (int bit = 31; bit >= 0; --bit) {
+        const uint32_t b = 1u << bit;
+        int cnt = 0;
+        for (int j = threadIdx.x; j < width; j += 256) {
+            int64_t idx = i - half + j;
+            idx = idx < 0 ? 0 : (idx >= (int64_t)n ? (int64_t)n - 1 : idx);
+            const uint32_t key = float_key(x[idx]);
+            cnt += ((key & mask) == prefix) && !(key & b);
+        }
+        for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = cnt;
+        __syncthreads();
+        const int zeros = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        __syncthreads();
+        if (k >= zeros) {
+            k -= zeros;
+            prefix |= b;
+        }
+        mask |= b;
+    }
+    if (threadIdx.x == 0) out[i] = key_float(prefix);
+}
+
+hipError_t launch_running_median(const float* x, uint64_t n, uint32_t width, float* out, uint64_t x_stride,
+                                 uint64_t out_stride, uint32_t batch, hipStream_t s)
+{
+    if (!n || !batch) return hipSuccess;
+    if (width <= (uint32_t)kRmedSmallMax) {
+        hipLaunchKernelGGL(rmed_small_kernel, dim3((uint32_t)((n + kRmedTile - 1) / kRmedTile), batch),
+                           dim3(kRmedTile), 0, s, x, n, (int)width, out, x_stride, out_stride);
+    } else {
+        hipLaunchKernelGGL(rmed_large_kernel, dim3((uint32_t)n, batch), dim3(256), 0, s, x, n, (int)width,
+                           out, x_stride, out_stride);
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Dereddening (time_series.py:93-122, running_medians.py:40-83)
+// ---------------------------------------------------------------------------
+// numpy float32 pairwise summation (the add-reduce inner loop used by
+// ndarray.mean over a contiguous axis): blocks of <= 128 with 8 accumulators,
+// recursive halving at multiples of 8 above that; the reduction starts from 0.
+__device__ float np_pairwise_leaf(const float* a, int n)
+{
+    if (n < 8) {
+        float r = 0.0f;
+        for (int i = 0; i < n; ++i) r = __fadd_rn(r, a[i]);
+        return r;
+    }
+    float r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
+    int i = 8;
+    for (; i < n - (n % 8); i += 8) {
+        r0 = __fadd_rn(r0, a[i + 0]); r1 = __fadd_rn(r1, a[i + 1]);
+        r2 = __fadd_rn(r2, a[i + 2]); r3 = __fadd_rn(r3, a[i + 3]);
+        r4 = __fadd_rn(r4, a[i + 4]); r5 = __fadd_rn(r5, a[i + 5]);
+        r6 = __fadd_rn(r6, a[i + 6]); r7 = __fadd_rn(r7, a[i + 7]);
+    }
+    float res = __fadd_rn(__fadd_rn(__fadd_rn(r0, r1), __fadd_rn(r2, r3)),
+                          __fadd_rn(__fadd_rn(r4, r5), __fadd_rn(r6, r7)));
+    for (; i < n; ++i) res = __fadd_rn(res, a[i]);
+    return res;
+}
+
+__device__ float np_pairwise_sum(const float* a, int n)
+{
+    if (n <= 128) return np_pairwise_leaf(a, n);
+    int offs[24], ns[24], st[24];
+    float left[24];
+    int sp = 0;
+    offs[0] = 0; ns[0] = n; st[0] = 0;
+    float ret = 0.0f;
+    while (sp >= 0) {
+        const int off = offs[sp], nn = ns[sp];
+        if (nn <= 128) {
+            ret = np_pairwise_leaf(a + off, nn);
+            --sp;
+            continue;
+        }
+        int n2 = nn / 2;
+        n2 -= n2 % 8;
+        if (st[sp] == 0) {
+            st[sp] = 1;
+            ++sp; offs[sp] = off; ns[sp] = n2; st[sp] = 0;
+        } else if (st[sp] == 1) {
+            left[sp] = ret;
+            st[sp] = 2;
+            ++sp; offs[sp] = off + n2; ns[sp] = nn - n2; st[sp] = 0;
+        } else {
+            ret = __fadd_rn(left[sp], ret);
+            --sp;
+        }
+    }
+    return ret;
+}
+
+// scrunch(): mean of consecutive blocks of `factor` samples; numpy divides the
+// float32 sum by an np.intp count, i.e. in float64, then casts to float32.
+__global__ __launch_bounds__(256) void scrunch_kernel(const float* __restrict__ x, uint64_t n_out, uint32_t factor,
+                                                      float* __restrict__ out, uint64_t x_stride, uint64_t out_stride)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_out) return;
+    x += (uint64_t)blockIdx.y * x_stride + i * factor;
+    out += (uint64_t)blockIdx.y * out_stride;
+    const float s = np_pairwise_sum(x, (int)factor);
+    out[i] = (float)((double)s / (double)factor);
+}
+
+hipError_t launch_scrunch(const float* x, uint64_t n_out, uint32_t factor, float* out, uint64_t x_stride,
+                          uint64_t out_stride, uint32_t batch, hipStream_t s)
+{
+    if (!n_out || !batch) return hipSuccess;
+    hipLaunchKernelGGL(scrunch_kernel, dim3((uint32_t)((n_out + 255) / 256), batch), dim3(256), 0, s,
+                       x, n_out, factor, out, x_stride, out_stride);
+    return hipGetLastError();
+}
+
+// np.interp(i, xp, fp) (compiled_base.c arr_interp) for xp[j] = j*factor +
+// (factor-1)/2, fp = rmed_lo: slope*(x - xp[j]) + fp[j], unfused, in float64.
+__device__ double np_interp_at(uint64_t i, const float* __restrict__ fp, uint64_t n_lo, uint32_t factor)
+{
+    const double c = 0.5 * ((double)factor - 1.0);
+    const double xv = (double)i;
+    auto xp = [&](int64_t j) { return (double)(j * (int64_t)factor) + c; };
+    const int64_t last = (int64_t)n_lo - 1;
+    if (n_lo == 1 || xv < xp(0)) return (double)fp[0];
+    if (xv > xp(last)) return (double)fp[last];
+    int64_t j = (int64_t)floor((xv - c) / (double)factor);
+    if (j < 0) j = 0;
+    if (j > last) j = last;
+    while (j > 0 && xp(j) > xv) --j;
+    while (j < last && xp(j + 1) <= xv) ++j;
+    if (j == last || xp(j) == xv) return (double)fp[j];
+    const double y0 = (double)fp[j], y1 = (double)fp[j + 1];
+    const double slope = __ddiv_rn(__dsub_rn(y1, y0), __dsub_rn(xp(j + 1), xp(j)));
+    return __dadd_rn(__dmul_rn(slope, __dsub_rn(xv, xp(j))), y0);
+}
+
+// out[i] = float32(x[i] - interp(i))  (time_series.py:118-122)
+__global__ __launch_bounds__(256) void deredden_subtract_kernel(const float* __restrict__ x, uint64_t n,
+                                                                const float* __restrict__ fp, uint64_t n_lo,
+                                                                uint32_t factor, float* __restrict__ out,
+                                                                uint64_t x_stride, uint64_t lo_stride,
+                                                                uint64_t out_stride)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    x += (uint64_t)blockIdx.y * x_stride;
+    fp += (uint64_t)blockIdx.y * lo_stride;
+    out += (uint64_t)blockIdx.y * out_stride;
+    out[i] = (float)__dsub_rn((double)x[i], np_interp_at(i, fp, n_lo, factor));
+}
+
+hipError_t launch_deredden_subtract(const float* x, uint64_t n, const float* rmed_lo, uint64_t n_lo,
+                                    uint32_t factor, float* out, uint64_t x_stride, uint64_t lo_stride,
+                                    uint64_t out_stride, uint32_t batch, hipStream_t s)
+{
+    if (!n || !batch) return hipSuccess;
+    hipLaunchKernelGGL(deredden_subtract_kernel, dim3((uint32_t)((n + 255) / 256), batch), dim3(256), 0, s,
+                       x, n, rmed_lo, n_lo, factor, out, x_stride, lo_stride, out_stride);
+    return hipGetLastError();
+}
+
+// fast_running_median output (running_medians.py:81-83): the interpolated
+// running median itself, float64.
+__global__ __launch_bounds__(256) void interp_kernel(uint64_t n, const float* __restrict__ fp, uint64_t n_lo,
+                                                     uint32_t factor, double* __restrict__ out)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = np_interp_at(i, fp, n_lo, factor);
+}
+
+hipError_t launch_interp(uint64_t n, const float* rmed_lo, uint64_t n_lo, uint32_t factor, double* out,
+                         hipStream_t s)
+{
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(interp_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, n, rmed_lo, n_lo,
+                       factor, out);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Normalisation (time_series.py:66-90): mean and variance in float64 (two
+// passes, as numpy's var), then float32((x - mean) / sqrt(var)).
+// ---------------------------------------------------------------------------
+constexpr int kNormBlock = 256;
+
+__device__ __forceinline__ double block_sum_d(double v, double* sh)
+{
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double t = 0.0;
+    if (threadIdx.x == 0) t = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+    __syncthreads();
+    return t;
+}
+
+// mode 0: partial sums of x; mode 1: partial sums of (x - mean)^2, mean = stats[2*b]
+__global__ __launch_bounds__(kNormBlock) void norm_partial_kernel(const float* __restrict__ x, uint64_t n,
+                                                                  uint64_t x_stride, double* __restrict__ partials,
+                                                                  const double* __restrict__ stats, int mode)
+{
+    __shared__ double sh[4];
+    x += (uint64_t)blockIdx.y * x_stride;
+    const double mean = mode ? stats[2 * blockIdx.y] : 0.0;
+    double acc = 0.0;
+    for (uint64_t i = (uint64_t)blockIdx.x * kNormBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kNormBlock) {
+        const double v = (double)x[i];
+        if (mode) {
+            const double d = v - mean;
+            acc += d * d;
+        } else {
+            acc += v;
+        }
+    }
+    const double t = block_sum_d(acc, sh);
+    if (threadIdx.x == 0) partials[(uint64_t)blockIdx.y * gridDim.x + blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(kNormBlock) void norm_finalize_kernel(const double* __restrict__ partials, uint32_t nblocks,
+                                                                   uint64_t n, double* __restrict__ stats, int mode)
+{
+    __shared__ double sh[4];
+    double acc = 0.0;
+    for (uint32_t i = threadIdx.x; i < nblocks; i += kNormBlock) acc += partials[(uint64_t)blockIdx.x * nblocks + i];
+    const double t = block_sum_d(acc, sh);
+    if (threadIdx.x == 0) stats[2 * blockIdx.x + mode] = t / (double)n;
+}
+
+__global__ __launch_bounds__(256) void norm_apply_kernel(const float* __restrict__ x, uint64_t n,
+                                                         const double* __restrict__ stats, float* __restrict__ out,
+                                                         uint64_t x_stride, uint64_t out_stride)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const double mean = stats[2 * blockIdx.y], var = stats[2 * blockIdx.y + 1];
+    const double norm = sqrt(var);
+    out[(uint64_t)blockIdx.y * out_stride + i] =
+        (float)__ddiv_rn(__dsub_rn((double)x[(uint64_t)blockIdx.y * x_stride + i], mean), norm);
+}
+
+// d_partials must hold batch * nblocks + 2 * batch doubles.
+hipError_t launch_normalise(const float* x, uint64_t n, float* out, double* d_partials, uint32_t nblocks,
+                            uint64_t x_stride, uint64_t out_stride, uint32_t batch, hipStream_t s)
+{
+    if (!n || !batch) return hipSuccess;
+    double* stats = d_partials + (uint64_t)batch * nblocks;
+    for (int mode = 0; mode < 2; ++mode) {
+        hipLaunchKernelGGL(norm_partial_kernel, dim3(nblocks, batch), dim3(kNormBlock), 0, s, x, n, x_stride,
+                           d_partials, stats, mode);
+        hipLaunchKernelGGL(norm_finalize_kernel, dim3(batch), dim3(kNormBlock), 0, s, d_partials, nblocks, n,
+                           stats, mode);
+    }
+    hipLaunchKernelGGL(norm_apply_kernel, dim3((uint32_t)((n + 255) / 256), batch), dim3(256), 0, s, x, n, stats,
+                       out, x_stride, out_stride);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Kernel-API helpers (kernels.hpp:19-38, :73-101)
+// ---------------------------------------------------------------------------
+// out[i] = (y ? x[i] + y[(i + shift) mod n] : x[(i + shift) mod n])
+__global__ __launch_bounds__(256) void rollback_kernel(const float* __restrict__ x, uint64_t n, uint64_t shift,
+                                                       const float* __restrict__ y, float* __restrict__ out)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint64_t j = i + shift % n;
+    if (j >= n) j -= n;
+    out[i] = y ? __fadd_rn(x[i], y[j]) : x[j];
+}
+
+hipError_t launch_rollback(const float* x, uint64_t n, uint64_t shift, const float* y, float* out, hipStream_t s)
+{
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(rollback_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, x, n, shift, y, out);
+    return hipGetLastError();
+}
+
+// One wave: fp64 prefix over the first min(n, nsum) elements.
+__global__ __launch_bounds__(64) void cps_scan_kernel(const float* __restrict__ x, uint64_t n, uint64_t nsum,
+                                                      float* __restrict__ out, float* __restrict__ total)
+{
+    const int lane = threadIdx.x;
+    const uint64_t c = (n + 63) / 64;
+    const uint64_t j0 = min((uint64_t)lane * c, n), j1 = min(j0 + c, n);
+    double part = 0.0;
+    for (uint64_t j = j0; j < j1; ++j) part += (double)x[j];
+    const double incl = wave_scan_d(part, lane);
+    double acc = __shfl_up(incl, 1, 64);
+    if (lane == 0) acc = 0.0;
+    for (uint64_t j = j0; j < j1; ++j) {
+        acc += (double)x[j];
+        if (j < nsum) out[j] = (float)acc;
+    }
+    const float t = __shfl((float)acc, (int)((n - 1) / c), 64);
+    if (lane == 0) *total = t;
+}
+
+__global__ __launch_bounds__(256) void cps_wrap_kernel(uint64_t n, uint64_t nsum, float* __restrict__ out,
+                                                       const float* __restrict__ total)
+{
+    const uint64_t i = n + (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= nsum) return;
+    const uint64_t q = i / n;
+    out[i] = __fadd_rn(out[i - q * n], __fmul_rn((float)q, *total));
+}
+
+hipError_t launch_circular_prefix_sum(const float* x, uint64_t n, uint64_t nsum, float* out, hipStream_t s)
+{
+    if (!n || !nsum) return hipSuccess;
+    float* total = out + nsum;   // caller provides one extra float
+    hipLaunchKernelGGL(cps_scan_kernel, dim3(1), dim3(64), 0, s, x, n, nsum, out, total);
+    if (nsum > n)
+        hipLaunchKernelGGL(cps_wrap_kernel, dim3((uint32_t)((nsum - n + 255) / 256)), dim3(256), 0, s, n, nsum,
+                           out, total);
+    return hipGetLastError();
+}
+
+}  // namespace rt

@@ -1,0 +1,948 @@
+// C ABI of the engine (include/riptide_amd.h): host-buffer drop-ins for
+// riptide.libcpp and the device-resident batched periodogram.
+#include "riptide_amd.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "kernels.hpp"
+#include "plan.hpp"
+
+using namespace rt;
+
+namespace {
+
+thread_local std::string g_err;
+thread_local int g_device = 0;
+
+int fail(int code, const std::string& msg)
+{
+    g_err = msg;
+    return code;
+}
+
+struct HipError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+inline void ck(hipError_t e, const char* what)
+{
+    if (e != hipSuccess) throw HipError(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// Exception barrier for every entry point.
+template <class F>
+int guarded(F&& f)
+{
+    try {
+        return f();
+    } catch (const std::invalid_argument& e) {
+        return fail(RT_EINVAL, e.what());
+    } catch (const HipError& e) {
+        return fail(RT_EHIP, e.what());
+    } catch (const std::exception& e) {
+        return fail(RT_EINTERNAL, e.what());
+    } catch (...) {
+        return fail(RT_EINTERNAL, "unknown error");
+    }
+}
+
+// ---- per-device context for host-buffer calls: stream + grow-only buffers
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    void* get(size_t n)
+    {
+        if (n > bytes) {
+            if (p) (void)hipFree(p);
+            p = nullptr;
+            bytes = 0;
+            ck(hipMalloc(&p, std::max<size_t>(n, 256)), "hipMalloc");
+            bytes = std::max<size_t>(n, 256);
+        }
+        return p;
+    }
+};
+
+struct Context {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    DevBuf buf[6];
+};
+
+std::mutex g_mu;
+std::vector<Context*> g_ctx;
+
+Context& context()
+{
+    ck(hipSetDevice(g_device), "hipSetDevice");
+    if ((int)g_ctx.size() <= g_device) g_ctx.resize(g_device + 1, nullptr);
+    if (!g_ctx[g_device]) {
+        Context* c = new Context();
+        c->device = g_device;
+        ck(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
+        g_ctx[g_device] = c;
+    }
+    return *g_ctx[g_device];
+}
+
+template <class T>
+T* dev(Context& c, int slot, size_t count)
+{
+    return (T*)c.buf[slot].get(count * sizeof(T));
+}
+
+void h2d(void* d, const void* h, size_t bytes, hipStream_t s)
+{
+    if (bytes) ck(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D");
+}
+
+void d2h(void* h, const void* d, size_t bytes, hipStream_t s)
+{
+    if (bytes) ck(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s), "hipMemcpyAsync D2H");
+}
+
+void sync(hipStream_t s) { ck(hipStreamSynchronize(s), "hipStreamSynchronize"); }
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// ---- profiling of cone / downsample launches
+struct ProfRec {
+    hipEvent_t a, b;
+    double alg, moved;
+};
+struct Profiler {
+    bool on = false;
+    std::vector<ProfRec> rec[2];
+    std::vector<hipEvent_t> pool;
+    hipEvent_t ev()
+    {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e;
+        ck(hipEventCreate(&e), "hipEventCreate");
+        return e;
+    }
+} g_prof;
+
+// ---- a compiled plan resident on one device
+struct DevicePlan {
+    std::vector<FfaXform> xf;
+    ExecPlan ex;
+    FfaXform* d_xf = nullptr;
+    ConeItem* d_items = nullptr;
+    int device = 0;
+    ~DevicePlan()
+    {
+        if (d_xf) (void)hipFree(d_xf);
+        if (d_items) (void)hipFree(d_items);
+    }
+    void upload()
+    {
+        ck(hipGetDevice(&device), "hipGetDevice");
+        ck(hipMalloc(&d_xf, std::max<size_t>(1, ex.xf.size()) * sizeof(FfaXform)), "hipMalloc");
+        ck(hipMalloc(&d_items, std::max<size_t>(1, ex.items.size()) * sizeof(ConeItem)), "hipMalloc");
+        if (!ex.xf.empty())
+            ck(hipMemcpy(d_xf, ex.xf.data(), ex.xf.size() * sizeof(FfaXform), hipMemcpyHostToDevice), "upload xf");
+        if (!ex.items.empty())
+            ck(hipMemcpy(d_items, ex.items.data(), ex.items.size() * sizeof(ConeItem), hipMemcpyHostToDevice),
+               "upload items");
+    }
+};
+
+// Run all cone launches of an exec plan.
+void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStream_t s)
+{
+    a.xf = P.d_xf;
+    for (const Launch& L : P.ex.launches) {
+        a.items = P.d_items + L.first;
+        a.num_items = L.count;
+        ProfRec r{};
+        if (g_prof.on) {
+            r.a = g_prof.ev();
+            r.b = g_prof.ev();
+            r.alg = L.alg_bytes * batch;
+            r.moved = L.moved_bytes * batch;
+            ck(hipEventRecord(r.a, s), "hipEventRecord");
+        }
+        ck(launch_cone(a, batch, s), "cone_kernel");
+        if (g_prof.on) {
+            ck(hipEventRecord(r.b, s), "hipEventRecord");
+            g_prof.rec[0].push_back(r);
+        }
+    }
+}
+
+// Single-transform FFA (ffa2 / benchmark_ffa2): in (device) -> out (device).
+void ffa_device(const float* d_in, size_t rows, size_t cols, float* d_out, float* d_tmp, hipStream_t s,
+                DevicePlan* cached = nullptr)
+{
+    if (!rows || !cols) return;
+    if (lds_row_capacity((uint32_t)cols) >= 3) {
+        DevicePlan local;
+        DevicePlan& P = cached ? *cached : local;
+        if (!cached || P.ex.launches.empty()) {
+            FfaXform X{};
+            X.p = (uint32_t)cols;
+            X.m = (uint32_t)rows;
+            build_exec_plan({X}, false, 0, ~0ull, P.ex);
+            P.upload();
+        }
+        ConeArgs a{};
+        a.leaves = d_in;
+        a.ping = d_out;
+        a.pong = d_tmp;
+        int* flag = nullptr;
+        a.error_flag = flag;
+        run_cone_launches(P, a, 1, s);
+        return;
+    }
+    // rows too wide for LDS: per-depth global-memory passes
+    int depth = 0;
+    while ((1ull << depth) < rows) ++depth;
+    std::vector<std::vector<uint2>> levels(depth + 1);
+    levels[0].push_back(make_uint2(0, (uint32_t)rows));
+    for (int d = 0; d < depth; ++d)
+        for (const uint2& n : levels[d]) {
+            if (n.y <= 1) { levels[d + 1].push_back(n); continue; }
+            const uint32_t h = n.y >> 1;
+            levels[d + 1].push_back(make_uint2(n.x, h));
+            levels[d + 1].push_back(make_uint2(n.x + h, n.y - h));
+        }
+    uint2* d_nodes = nullptr;
+    ck(hipMalloc(&d_nodes, std::max<size_t>(1, rows) * sizeof(uint2)), "hipMalloc");
+    const float* src = d_in;
+    for (int d = depth - 1; d >= 0; --d) {
+        float* dst = ((d % 2) == 0) ? d_out : d_tmp;
+        ck(hipMemcpyAsync(d_nodes, levels[d].data(), levels[d].size() * sizeof(uint2), hipMemcpyHostToDevice, s),
+           "nodes");
+        ck(launch_ffa_level(src, dst, d_nodes, (uint32_t)levels[d].size(), (uint32_t)rows, (uint32_t)cols, s),
+           "ffa_level");
+        ck(hipStreamSynchronize(s), "sync");
+        src = dst;
+    }
+    if (depth == 0) ck(hipMemcpyAsync(d_out, d_in, rows * cols * 4, hipMemcpyDeviceToDevice, s), "copy");
+    ck(hipStreamSynchronize(s), "sync");
+    (void)hipFree(d_nodes);
+}
+
+void check_widths(const uint64_t* w, size_t nw, size_t bins)
+{
+    for (size_t i = 0; i < nw; ++i)
+        if (!(w[i] > 0 && w[i] < bins)) throw std::invalid_argument("trial widths must be all > 0 and < columns");
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// periodogram plan
+// ---------------------------------------------------------------------------
+struct rt_plan {
+    PgramPlan pg;
+    DevicePlan dp;
+    std::vector<uint32_t> widths;
+    std::vector<DsRung> rungs;
+    DsRung* d_rungs = nullptr;
+    uint32_t ds_blocks = 0;
+    ~rt_plan()
+    {
+        if (d_rungs) (void)hipFree(d_rungs);
+    }
+};
+
+namespace {
+
+rt_plan* make_plan(size_t size, double tsamp, const uint64_t* widths, size_t nw, double pmin, double pmax,
+                   size_t bmin, size_t bmax)
+{
+    PgramParams prm;
+    prm.size = size;
+    prm.tsamp = tsamp;
+    prm.pmin = pmin;
+    prm.pmax = pmax;
+    prm.bmin = bmin;
+    prm.bmax = bmax;
+    const std::string msg = check_pgram_args(prm);
+    if (!msg.empty()) throw std::invalid_argument(msg);
+    if (nw > (size_t)kMaxWidths) throw std::invalid_argument("at most 32 trial widths are supported");
+    check_widths(widths, nw, bmin);
+    if (lds_row_capacity((uint32_t)bmax) < 3) throw std::invalid_argument("bins_max too large for the LDS FFA engine");
+    auto* P = new rt_plan();
+    try {
+        build_pgram_plan(prm, P->pg);
+        P->widths.assign(widths, widths + nw);
+        std::vector<FfaXform> xf;
+        for (const Step& s : P->pg.steps) {
+            if (!s.rows_eval) continue;   // nothing of this transform reaches the output
+            FfaXform X{};
+            X.p = s.bins;
+            X.m = s.rows;
+            X.rows_eval = s.rows_eval;
+            X.rung = s.rung;
+            X.src_off = P->pg.rungs[s.rung].leaf_off;
+            X.snr_row = s.out_row;
+            X.stdnoise = s.stdnoise;
+            xf.push_back(X);
+        }
+        // scratch budget per ping/pong buffer and trial: 32 M floats (128 MiB)
+        build_exec_plan(xf, true, (uint32_t)nw, 32ull << 20, P->dp.ex);
+        P->dp.upload();
+        // downsample ladder over the rungs that feed at least one transform
+        std::vector<bool> used(P->pg.rungs.size(), false);
+        for (const FfaXform& X : xf) used[X.rung] = true;
+        uint32_t blocks = 0;
+        for (size_t r = 0; r < P->pg.rungs.size(); ++r) {
+            if (!used[r]) continue;
+            const Rung& R = P->pg.rungs[r];
+            DsRung d{};
+            d.f = R.f;
+            d.n = R.n;
+            d.out_off = R.leaf_off;
+            d.first_block = blocks;
+            d.identity = R.f == 1.0;
+            blocks += (uint32_t)((R.n + 255) / 256);
+            P->rungs.push_back(d);
+        }
+        P->ds_blocks = blocks;
+        ck(hipMalloc(&P->d_rungs, std::max<size_t>(1, P->rungs.size()) * sizeof(DsRung)), "hipMalloc");
+        if (!P->rungs.empty())
+            ck(hipMemcpy(P->d_rungs, P->rungs.data(), P->rungs.size() * sizeof(DsRung), hipMemcpyHostToDevice),
+               "upload rungs");
+    } catch (...) {
+        delete P;
+        throw;
+    }
+    return P;
+}
+
+size_t plan_ws_bytes(const rt_plan* P, size_t batch)
+{
+    size_t b = align_up(P->pg.leaf_floats * 4 * batch, 256);
+    b += 2 * align_up(P->dp.ex.scratch_floats * 4 * batch, 256);
+    b += 256;   // error flag
+    return b;
+}
+
+void run_periodogram(const rt_plan* P, const float* d_data, size_t batch, size_t data_stride, float* d_snrs,
+                     size_t snr_stride, void* ws, size_t ws_bytes, hipStream_t s)
+{
+    if (ws_bytes < plan_ws_bytes(P, batch)) throw std::invalid_argument("workspace too small");
+    char* w = (char*)ws;
+    float* leaves = (float*)w;
+    w += align_up(P->pg.leaf_floats * 4 * batch, 256);
+    float* ping = (float*)w;
+    w += align_up(P->dp.ex.scratch_floats * 4 * batch, 256);
+    float* pong = (float*)w;
+    w += align_up(P->dp.ex.scratch_floats * 4 * batch, 256);
+    int* flag = (int*)w;
+    ck(hipMemsetAsync(flag, 0, sizeof(int), s), "hipMemsetAsync");
+    ProfRec r{};
+    if (g_prof.on) {
+        r.a = g_prof.ev();
+        r.b = g_prof.ev();
+        ck(hipEventRecord(r.a, s), "hipEventRecord");
+    }
+    ck(launch_downsample_ladder(d_data, P->pg.prm.size, data_stride, P->d_rungs, (uint32_t)P->rungs.size(),
+                                P->ds_blocks, leaves, P->pg.leaf_floats, (uint32_t)batch, s),
+       "downsample_ladder");
+    if (g_prof.on) {
+        ck(hipEventRecord(r.b, s), "hipEventRecord");
+        double bytes = 0;
+        for (const DsRung& d : P->rungs) bytes += 4.0 * (double)d.n + (d.identity ? 4.0 * d.n : 4.0 * P->pg.prm.size);
+        r.alg = r.moved = bytes * batch;
+        g_prof.rec[1].push_back(r);
+    }
+    ConeArgs a{};
+    a.num_widths = (uint32_t)P->widths.size();
+    for (size_t i = 0; i < P->widths.size(); ++i) a.widths[i] = P->widths[i];
+    a.leaves = leaves;
+    a.leaves_stride = P->pg.leaf_floats;
+    a.ping = ping;
+    a.pong = pong;
+    a.buf_stride = P->dp.ex.scratch_floats;
+    a.snr = d_snrs;
+    a.snr_stride = snr_stride;
+    a.error_flag = flag;
+    run_cone_launches(P->dp, a, (uint32_t)batch, s);
+}
+
+// Dereddening + normalisation (device).  Workspace layout: [lores | rmed | partials]
+struct DeredGeom {
+    size_t sf = 1, n_lo = 0, rmed_w = 0;
+    size_t lores_floats = 0, rmed_floats = 0, partial_doubles = 0;
+};
+constexpr uint32_t kNormBlocks = 512;
+
+DeredGeom dered_geom(size_t size, size_t ws, size_t minpts, size_t batch, bool deredden)
+{
+    DeredGeom g;
+    if (deredden) {
+        if (!(minpts % 2)) throw std::invalid_argument("min_points must be an odd number");
+        const double q = (double)ws / (double)minpts;
+        g.sf = (size_t)std::max(1.0, q);
+        if (g.sf == 1) {
+            g.n_lo = size;
+            g.rmed_w = ws;
+        } else {
+            g.n_lo = size / g.sf;
+            g.rmed_w = minpts;
+            g.lores_floats = align_up(g.n_lo * batch, 64);
+        }
+        if (!(g.rmed_w % 2)) throw std::invalid_argument("width must be an odd number");
+        if (!(g.rmed_w < g.n_lo)) throw std::invalid_argument("width must be < size");
+        g.rmed_floats = align_up(g.n_lo * batch, 64);
+    }
+    g.partial_doubles = (size_t)kNormBlocks * batch + 2 * batch + 8;
+    return g;
+}
+
+size_t dered_ws_bytes(const DeredGeom& g)
+{
+    return (g.lores_floats + g.rmed_floats) * 4 + g.partial_doubles * 8 + 256;
+}
+
+void run_deredden_normalise(const float* d_in, size_t size, size_t batch, size_t in_stride, const DeredGeom& g,
+                            bool deredden, bool normalise, float* d_out, size_t out_stride, void* ws, hipStream_t s)
+{
+    float* lores = (float*)ws;
+    float* rmed = lores + g.lores_floats;
+    double* partials = (double*)align_up((size_t)(rmed + g.rmed_floats), 256);
+    const float* cur = d_in;
+    size_t cur_stride = in_stride;
+    if (deredden) {
+        const float* rin = d_in;
+        size_t rstride = in_stride;
+        if (g.sf > 1) {
+            ck(launch_scrunch(d_in, g.n_lo, (uint32_t)g.sf, lores, in_stride, g.n_lo, (uint32_t)batch, s), "scrunch");
+            rin = lores;
+            rstride = g.n_lo;
+        }
+        ck(launch_running_median(rin, g.n_lo, (uint32_t)g.rmed_w, rmed, rstride, g.n_lo, (uint32_t)batch, s),
+           "running_median");
+        ck(launch_deredden_subtract(d_in, size, rmed, g.n_lo, (uint32_t)g.sf, d_out, in_stride, g.n_lo, out_stride,
+                                    (uint32_t)batch, s),
+           "deredden_subtract");
+        cur = d_out;
+        cur_stride = out_stride;
+    }
+    if (normalise) {
+        ck(launch_normalise(cur, size, d_out, partials, kNormBlocks, cur_stride, out_stride, (uint32_t)batch, s),
+           "normalise");
+    } else if (!deredden && cur != d_out) {
+        for (size_t b = 0; b < batch; ++b)
+            ck(hipMemcpyAsync(d_out + b * out_stride, d_in + b * in_stride, size * 4, hipMemcpyDeviceToDevice, s),
+               "copy");
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// entry points
+// ---------------------------------------------------------------------------
+extern "C" {
+
+const char* rt_last_error(void) { return g_err.c_str(); }
+
+const char* rt_version(void) { return "riptide_amd 0.1.0 (gfx950)"; }
+
+int rt_set_device(int device)
+{
+    return guarded([&] {
+        ck(hipSetDevice(device), "hipSetDevice");
+        g_device = device;
+        return RT_OK;
+    });
+}
+
+int rt_rollback(const float* x, size_t size, size_t shift, float* out)
+{
+    return guarded([&] {
+        if (!size) return RT_OK;
+        std::lock_guard<std::mutex> lk(g_mu);
+        Context& c = context();
+        float* dx = dev<float>(c, 0, size);
+        float* dz = dev<float>(c, 1, size);
+        h2d(dx, x, size * 4, c.stream);
+        ck(launch_rollback(dx, size, shift, nullptr, dz, c.stream), "rollback");
+        d2h(out, dz, size * 4, c.stream);
+        sync(c.stream);
+        return RT_OK;
+    });
+}
+
+int rt_fused_rollback_add(const float* x, const float* y, size_t size, size_t shift, float* out)
+{
+    return guarded([&] {
+        if (!size) return RT_OK;
+        std::lock_guard<std::mutex> lk(g_mu);
+        Context& c = context();
+        float* dx = dev<float>(c, 0, size);
+        float* dy = dev<float>(c, 1, size);
+        float* dz = dev<float>(c, 2, size);
+        h2d(dx, x, size * 4, c.stream);
+        h2d(dy, y, size * 4, c.stream);
+        ck(launch_rollback(dx, size, shift, dy, dz, c.stream), "fused_rollback_add");
+        d2h(out, dz, size * 4, c.stream);
+        sync(c.stream);
+        return RT_OK;
+    });
+}
+
+int rt_circular_prefix_sum(const float* x, size_t size, size_t nsum, float* out)
+{
+    return guarded([&] {
+        if (!nsum) return RT_OK;
+        if (!size) throw std::invalid_argument("circular_prefix_sum of an empty array");
+        std::lock_guard<std::mutex> lk(g_mu);
+        Context& c = context();
+        float* dx = dev<float>(c, 0, size);
+        float* dz = dev<float>(c, 1, nsum + 1);
+        h2d(dx, x, size * 4, c.stream);
+        ck(launch_circular_prefix_sum(dx, size, nsum, dz, c.stream), "circular_prefix_sum");
+        d2h(out, dz, nsum * 4, c.stream);
+        sync(c.stream);
+        return RT_OK;
+    });
+}
+
+int rt_ffa2(const float* in, size_t rows, size_t cols, float* out)
+{
+    return guarded([&] {
+        if (!rows || !cols) return RT_OK;
+        if (rows > 0x7FFFFFFFull || rows * cols > (1ull << 40)) throw std::invalid_argument("ffa2 input too large");
+        std::lock_guard<std::mutex> lk(g_mu);
+        Context& c = context();
+        const size_t n = rows * cols;
+        float* dx = dev<float>(c, 0, n);
+        float* dz = dev<float>(c, 1, n);
+        float* dt = dev<float>(c, 2, n);
+        h2d(dx, in, n * 4, c.stream);
+        ffa_device(dx, rows, cols, dz, dt, c.stream);
+        d2h(out, dz, n * 4, c.stream);
+        sync(c.stream);
+        return RT_OK;
+    });
+}
+
+int rt_benchmark_ffa2(size_t rows, size_t cols, size_t loops, double* seconds)
+{
+    return guarded([&] {
+        *seconds = 0;
+        if (!rows || !cols || !loops) return RT_OK;
+        std::lock_guard<std::mutex> lk(g_mu);
+        Context& c = context();
+        const size_t n = rows * cols;
+        float* dx = dev<float>(c, 0, n);
+        float* dz = dev<float>(c, 1, n);
+        float* dt = dev<float>(c, 2, n);
+        ck(hipMemsetAsync(dx, 0, n * 4, c.stream), "memset");
+        DevicePlan P;
+        ffa_device(dx, rows, cols, dz, dt, c.stream, &P);   // warm-up + plan
+        hipEvent_t a, b;
+        ck(hipEventCreate(&a), "event");
+        ck(hipEventCreate(&b), "event");
+        ck(hipEventRecord(a, c.stream), "record");
+        for (size_t i = 0; i < loops; ++i) ffa_device(dx, rows, cols, dz, dt, c.stream, &P);
+        ck(hipEventRecord(b, c.stream), "record");
+        ck(hipEventSynchronize(b), "sync");
+        float ms = 0;
+        ck(hipEventElapsedTime(&ms, a, b), "elapsed");
+        (void)hipEventDestroy(a);
+        (void)hipEventDestroy(b);
+        *seconds = ms * 1e-3 / (double)loops;
+        return RT_OK;
+    });
+}
+
+int rt_snr2(const float* x, size_t rows, size_t cols, const uint64_t* widths, size_t nw, float stdnoise, float* out)
+{
+    return guarded([&] {
+        if (!(stdnoise > 0)) throw std::invalid_argument("stdnoise must be > 0");
+        check_widths(widths, nw, cols);
+        if (!rows || !nw) return RT_OK;
+        std::lock_guard<std::mutex> lk(g_mu);
+        Context& c = context();
+        const size_t n = rows * cols;
+        float* dx = dev<float>(c, 0, n);
+        float* dc = dev<float>(c, 1, n + rows);
+        uint32_t* dw = dev<uint32_t>(c, 2, nw);
+        float* dz = dev<float>(c, 3, rows * nw);
+        std::vector<uint32_t> w32(widths, widths + nw);
+        h2d(dx, x, n * 4, c.stream);
+        h2d(dw, w32.data(), nw * 4, c.stream);
+        ck(launch_snr_rows(dx, rows, (uint32_t)cols, dw, (uint32_t)nw, stdnoise, dc, dz, c.stream), "snr");
+        d2h(out, dz, rows * nw * 4, c.stream);
+        sync(c.stream);
+        return RT_OK;
+    });
+}
+
+int rt_snr1(const float* x, size_t size, const uint64_t* widths, size_t nw, float stdnoise, float* out)
+{
+    return rt_snr2(x, 1, size, widths, nw, stdnoise, out);
+}
+
+size_t rt_downsampled_size(size_t size, double f) { return downsampled_size(size, f); }
+
+int rt_downsample(const float* x, size_t size, double f, float* out)
+{
+    return guarded([&] {
+        // downsample.hpp:11-16
+        if (!((f > 1.0) & (f <= (double)size)))
+            throw std::invalid_argument("Downsampling factor must verify: 1 < f <= size");
+        const size_t n = downsampled_size(size, f);
+        std::lock_guard<std::mutex> lk(g_mu);
+        Context& c = context();
+        float* dx = dev<float>(c, 0, size);
+        float* dz = dev<float>(c, 1, n);
+        DsRung* dr = dev<DsRung>(c, 2, 1);
+        DsRung r{};
+        r.f = f;
+        r.n = n;
+        r.first_block = 0;
+        h2d(dx, x, size * 4, c.stream);
+        h2d(dr, &r, sizeof r, c.stream);
+        ck(launch_downsample_ladder(dx, size, size, dr, 1, (uint32_t)((n + 255) / 256), dz, n, 1, c.stream),
+           "downsample");
+        d2h(out, dz, n * 4, c.stream);
+        sync(c.stream);
+        return RT_OK;
+    });
+}
+
+int rt_periodogram_length(size_t size, double tsamp, double pmin, double pmax, size_t bmin, size_t bmax,
+                          size_t* length)
+{
+    return guarded([&] {
+        PgramParams prm;
+        prm.size = size;
+        prm.tsamp = tsamp;
+        prm.pmin = pmin;
+        prm.pmax = pmax;
+        prm.bmin = bmin;
+        prm.bmax = bmax;
+        const std::string msg = check_pgram_args(prm);
+        if (!msg.empty()) throw std::invalid_argument(msg);
+        PgramPlan pg;
+        build_pgram_plan(prm, pg);
+        *length = pg.length;
+        return RT_OK;
+    });
+}
+
+int rt_periodogram(const float* data, size_t size, double tsamp, const uint64_t* widths, size_t nw, double pmin,
+                   double pmax, size_t bmin, size_t bmax, double* periods, uint32_t* foldbins, float* snrs)
+{
+    return guarded([&] {
+        std::lock_guard<std::mutex> lk(g_mu);
+        Context& c = context();
+        rt_plan* P = make_plan(size, tsamp, widths, nw, pmin, pmax, bmin, bmax);
+        std::unique_ptr<rt_plan> hold(P);
+        fill_grid(P->pg, periods, foldbins);
+        const size_t L = P->pg.length;
+        if (!L) return RT_OK;
+        float* dx = dev<float>(c, 0, size);
+        float* dz = dev<float>(c, 1, std::max<size_t>(1, L * nw));
+        void* ws = c.buf[2].get(plan_ws_bytes(P, 1));
+        h2d(dx, data, size * 4, c.stream);
+        run_periodogram(P, dx, 1, size, dz, L * nw, ws, plan_ws_bytes(P, 1), c.stream);
+        int flag = 0;
+        char* w = (char*)ws + plan_ws_bytes(P, 1) - 256;
+        d2h(&flag, w, sizeof flag, c.stream);
+        d2h(snrs, dz, L * nw * 4, c.stream);
+        sync(c.stream);
+        if (flag) throw std::runtime_error("cone kernel: work item exceeded the LDS budget");
+        return RT_OK;
+    });
+}
+
+int rt_running_median(const float* x, size_t size, size_t width, float* out)
+{
+    return guarded([&] {
+        // running_median.hpp:103-107
+        if (!(width % 2)) throw std::invalid_argument("width must be an odd number");
+        if (!(width < size)) throw std::invalid_argument("width must be < size");
+        std::lock_guard<std::mutex> lk(g_mu);
+        Context& c = context();
+        float* dx = dev<float>(c, 0, size);
+        float* dz = dev<float>(c, 1, size);
+        h2d(dx, x, size * 4, c.stream);
+        ck(launch_running_median(dx, size, (uint32_t)width, dz, size, size, 1, c.stream), "running_median");
+        d2h(out, dz, size * 4, c.stream);
+        sync(c.stream);
+        return RT_OK;
+    });
+}
+
+int rt_fast_running_median(const float* x, size_t size, size_t ws, size_t minpts, double* out)
+{
+    return guarded([&] {
+        const DeredGeom g = dered_geom(size, ws, minpts, 1, true);
+        if (g.sf == 1) throw std::invalid_argument("scrunch factor is 1: use rt_running_median");
+        std::lock_guard<std::mutex> lk(g_mu);
+        Context& c = context();
+        float* dx = dev<float>(c, 0, size);
+        double* dz = dev<double>(c, 1, size);
+        float* lores = dev<float>(c, 2, g.n_lo);
+        float* rmed = dev<float>(c, 3, g.n_lo);
+        h2d(dx, x, size * 4, c.stream);
+        ck(launch_scrunch(dx, g.n_lo, (uint32_t)g.sf, lores, size, g.n_lo, 1, c.stream), "scrunch");
+        ck(launch_running_median(lores, g.n_lo, (uint32_t)g.rmed_w, rmed, g.n_lo, g.n_lo, 1, c.stream),
+           "running_median");
+        ck(launch_interp(size, rmed, g.n_lo, (uint32_t)g.sf, dz, c.stream), "interp");
+        d2h(out, dz, size * 8, c.stream);
+        sync(c.stream);
+        return RT_OK;
+    });
+}
+
+int rt_deredden_normalise(const float* x, size_t size, size_t ws, size_t minpts, int deredden, int normalise,
+                          float* out)
+{
+    return guarded([&] {
+        const DeredGeom g = dered_geom(size, ws, minpts, 1, deredden != 0);
+        std::lock_guard<std::mutex> lk(g_mu);
+        Context& c = context();
+        float* dx = dev<float>(c, 0, size);
+        float* dz = dev<float>(c, 1, size);
+        void* w = c.buf[2].get(dered_ws_bytes(g));
+        h2d(dx, x, size * 4, c.stream);
+        run_deredden_normalise(dx, size, 1, size, g, deredden != 0, normalise != 0, dz, size, w, c.stream);
+        d2h(out, dz, size * 4, c.stream);
+        sync(c.stream);
+        return RT_OK;
+    });
+}
+
+int rt_periodogram_grid(size_t size, double tsamp, double pmin, double pmax, size_t bmin, size_t bmax,
+                        double* periods, uint32_t* foldbins)
+{
+    return guarded([&] {
+        PgramParams prm;
+        prm.size = size;
+        prm.tsamp = tsamp;
+        prm.pmin = pmin;
+        prm.pmax = pmax;
+        prm.bmin = bmin;
+        prm.bmax = bmax;
+        const std::string msg = check_pgram_args(prm);
+        if (!msg.empty()) throw std::invalid_argument(msg);
+        PgramPlan pg;
+        build_pgram_plan(prm, pg);
+        fill_grid(pg, periods, foldbins);
+        return RT_OK;
+    });
+}
+
+int rt_schedule_check(size_t size, double tsamp, size_t nw, double pmin, double pmax, size_t bmin, size_t bmax,
+                      uint64_t* transforms, uint64_t* items, uint64_t* launches, double* alg_bytes,
+                      double* moved_bytes, uint64_t* cells)
+{
+    return guarded([&] {
+        PgramParams prm;
+        prm.size = size;
+        prm.tsamp = tsamp;
+        prm.pmin = pmin;
+        prm.pmax = pmax;
+        prm.bmin = bmin;
+        prm.bmax = bmax;
+        const std::string msg = check_pgram_args(prm);
+        if (!msg.empty()) throw std::invalid_argument(msg);
+        PgramPlan pg;
+        build_pgram_plan(prm, pg);
+        std::vector<FfaXform> xf;
+        for (const Step& s : pg.steps) {
+            if (!s.rows_eval) continue;
+            FfaXform X{};
+            X.p = s.bins;
+            X.m = s.rows;
+            X.rows_eval = s.rows_eval;
+            X.snr_row = s.out_row;
+            xf.push_back(X);
+        }
+        ExecPlan ex;
+        build_exec_plan(xf, true, (uint32_t)nw, 32ull << 20, ex);
+        // invariants: within every launch, each transform's items write disjoint
+        // row ranges, every item fits the LDS budget, and the last pass of every
+        // transform covers rows [0, m) exactly once.
+        std::vector<uint64_t> covered(ex.xf.size(), 0);
+        std::vector<uint32_t> last_pass(ex.xf.size(), 0);
+        for (const Launch& L : ex.launches)
+            for (uint32_t i = L.first; i < L.first + L.count; ++i) {
+                const ConeItem& it = ex.items[i];
+                last_pass[it.xform] = std::max(last_pass[it.xform], L.pass);
+            }
+        uint64_t a = 0;
+        double alg = 0, mv = 0;
+        for (const Launch& L : ex.launches) {
+            alg += L.alg_bytes;
+            mv += L.moved_bytes;
+            if (L.pass == 0) a += L.cells;
+            for (uint32_t i = L.first; i < L.first + L.count; ++i) {
+                const ConeItem& it = ex.items[i];
+                const FfaXform& X = ex.xf[it.xform];
+                if (it.s1 <= it.s0 || it.s1 > it.node_size || it.node_start + it.node_size > X.m)
+                    throw std::runtime_error("schedule: tile outside its node");
+                if (it.mode == kModeTile) {
+                    const ConeNeed n = cone_need(it.node_size, it.s0, it.s1, it.levels, X.p);
+                    if (n.max_rows > kMaxRows || n.max_floats > kLdsDataFloats || n.ranges > kMaxRanges)
+                        throw std::runtime_error("schedule: tile exceeds the LDS budget");
+                } else if ((int)it.node_size * (int)X.p > kLdsDataFloats || it.node_size > (uint32_t)kMaxRows) {
+                    throw std::runtime_error("schedule: whole node exceeds the LDS budget");
+                }
+                if (L.pass == last_pass[it.xform]) {
+                    if (it.dst != kSelSnr || it.node_start != 0) throw std::runtime_error("schedule: bad final pass");
+                    covered[it.xform] += it.s1 - it.s0;
+                }
+            }
+        }
+        for (size_t t = 0; t < ex.xf.size(); ++t)
+            if (covered[t] != ex.xf[t].m) throw std::runtime_error("schedule: final pass does not cover the transform");
+        *transforms = ex.xf.size();
+        *items = ex.items.size();
+        *launches = ex.launches.size();
+        *alg_bytes = alg;
+        *moved_bytes = mv;
+        *cells = a;
+        return RT_OK;
+    });
+}
+
+int rt_plan_create(size_t size, double tsamp, const uint64_t* widths, size_t nw, double pmin, double pmax,
+                   size_t bmin, size_t bmax, rt_plan** plan)
+{
+    return guarded([&] {
+        ck(hipSetDevice(g_device), "hipSetDevice");
+        *plan = make_plan(size, tsamp, widths, nw, pmin, pmax, bmin, bmax);
+        return RT_OK;
+    });
+}
+
+void rt_plan_destroy(rt_plan* plan) { delete plan; }
+
+int rt_plan_shape(const rt_plan* P, size_t* length, size_t* nw)
+{
+    *length = P->pg.length;
+    *nw = P->widths.size();
+    return RT_OK;
+}
+
+int rt_plan_grid(const rt_plan* P, double* periods, uint32_t* foldbins)
+{
+    return guarded([&] {
+        fill_grid(P->pg, periods, foldbins);
+        return RT_OK;
+    });
+}
+
+int rt_plan_workspace_bytes(const rt_plan* P, size_t batch, size_t* bytes)
+{
+    *bytes = plan_ws_bytes(P, batch);
+    return RT_OK;
+}
+
+int rt_periodogram_device(const rt_plan* P, const float* d_data, size_t batch, size_t data_stride, float* d_snrs,
+                          size_t snr_stride, void* ws, size_t ws_bytes, void* stream)
+{
+    return guarded([&] {
+        if (!batch || !P->pg.length) return RT_OK;
+        run_periodogram(P, d_data, batch, data_stride, d_snrs, snr_stride, ws, ws_bytes, (hipStream_t)stream);
+        return RT_OK;
+    });
+}
+
+int rt_deredden_workspace_bytes(size_t size, size_t ws, size_t minpts, size_t batch, size_t* bytes)
+{
+    return guarded([&] {
+        *bytes = dered_ws_bytes(dered_geom(size, ws, minpts, batch, true));
+        return RT_OK;
+    });
+}
+
+int rt_deredden_normalise_device(const float* d_in, size_t size, size_t batch, size_t in_stride, size_t ws,
+                                 size_t minpts, int deredden, int normalise, float* d_out, size_t out_stride,
+                                 void* d_ws, size_t ws_bytes, void* stream)
+{
+    return guarded([&] {
+        const DeredGeom g = dered_geom(size, ws, minpts, batch, deredden != 0);
+        if (ws_bytes < dered_ws_bytes(g)) throw std::invalid_argument("workspace too small");
+        if (deredden && d_in == d_out) throw std::invalid_argument("deredden cannot run in place");
+        run_deredden_normalise(d_in, size, batch, in_stride, g, deredden != 0, normalise != 0, d_out, out_stride,
+                               d_ws, (hipStream_t)stream);
+        return RT_OK;
+    });
+}
+
+int rt_profile_enable(int on)
+{
+    g_prof.on = on != 0;
+    return RT_OK;
+}
+
+int rt_profile_reset(void)
+{
+    return guarded([&] {
+        for (auto& v : g_prof.rec)
+            for (auto& r : v) {
+                g_prof.pool.push_back(r.a);
+                g_prof.pool.push_back(r.b);
+            }
+        g_prof.rec[0].clear();
+        g_prof.rec[1].clear();
+        return RT_OK;
+    });
+}
+
+int rt_profile_read(int kind, double* ms, double* alg, double* moved, uint64_t* launches)
+{
+    return guarded([&] {
+        if (kind < 0 || kind > 1) throw std::invalid_argument("kind must be 0 or 1");
+        double t = 0, b = 0, mv = 0;
+        for (auto& r : g_prof.rec[kind]) {
+            ck(hipEventSynchronize(r.b), "hipEventSynchronize");
+            float e = 0;
+            ck(hipEventElapsedTime(&e, r.a, r.b), "hipEventElapsedTime");
+            t += e;
+            b += r.alg;
+            mv += r.moved;
+        }
+        *ms = t;
+        *alg = b;
+        *moved = mv;
+        *launches = g_prof.rec[kind].size();
+        return RT_OK;
+    });
+}
+
+int rt_plan_stats(const rt_plan* P, uint64_t* transforms, uint64_t* items, uint64_t* launches, double* alg,
+                  double* moved, uint64_t* cells)
+{
+    *transforms = P->dp.ex.xf.size();
+    *items = P->dp.ex.items.size();
+    *launches = P->dp.ex.launches.size();
+    double a = 0, m = 0;
+    uint64_t c = 0;
+    for (const Launch& L : P->dp.ex.launches) {
+        a += L.alg_bytes;
+        m += L.moved_bytes;
+        if (L.pass == 0) c += L.cells;
+    }
+    *alg = a;
+    *moved = m;
+    *cells = c;
+    return RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,472 @@
+// FFA periodogram hot path for MI355X (gfx950): downsampling ladder, LDS cone
+// kernel (several FFA merge levels per HBM pass), fused boxcar S/N epilogue.
+//
+// Exactness: every float operation that the reference performs is performed
+// here on the same operands in the same association (explicit *_rn intrinsics
+// where hipcc would otherwise contract into FMA), so the FFA transform is
+// bit-identical to riptide::transform (transforms.hpp:30-61) and downsample is
+// bit-identical to the strict restatement of downsample.hpp:44-82.
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace rt {
+
+// ---------------------------------------------------------------------------
+// Downsampling ladder (downsample.hpp:44-82; periodogram.hpp:162-168)
+// ---------------------------------------------------------------------------
+// One thread per output sample of one rung of one trial.  Rungs are flattened
+// along blockIdx.x through a per-rung first-block table; blockIdx.y = trial.
+__global__ __launch_bounds__(256) void downsample_ladder_kernel(
+    const float* __restrict__ x, uint64_t n_in, uint64_t x_stride,
+    const DsRung* __restrict__ rungs, uint32_t num_rungs,
+    float* __restrict__ out, uint64_t out_stride)
+{
+    uint32_t lo = 0, hi = num_rungs - 1;
+    const uint32_t b = blockIdx.x;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (rungs[mid].first_block <= b) lo = mid; else hi = mid - 1;
+    }
+    const DsRung r = rungs[lo];
+    const uint64_t k = (uint64_t)(b - r.first_block) * 256 + threadIdx.x;
+    if (k >= r.n) return;
+    x += (uint64_t)blockIdx.y * x_stride;
+    out += (uint64_t)blockIdx.y * out_stride + r.out_off;
+    if (r.identity) {           // f == 1: the rung searches the data at its own resolution
+        out[k] = x[k];
+        return;
+    }
+    const double f = r.f;
+    const double start = __dmul_rn((double)k, f);
+    const double end = __dadd_rn(start, f);
+    const uint64_t imin = (uint64_t)floor(start);
+    double dmax = floor(end);
+    const double last = (double)n_in - 1.0;
+    if (dmax > last) dmax = last;
+    const uint64_t imax = (uint64_t)dmax;
+    const float wmin = (float)__dsub_rn((double)(imin + 1), start);
+    const float wmax = (float)__dsub_rn(end, (double)imax);
+    float acc = __fmul_rn(wmin, x[imin]);
+    for (uint64_t i = imin + 1; i < imax; ++i)
+        acc = __fadd_rn(acc, x[i]);
+    acc = __fadd_rn(acc, __fmul_rn(wmax, x[imax]));
+    out[k] = acc;
+}
+
+hipError_t launch_downsample_ladder(const float* x, uint64_t n_in, uint64_t x_stride,
+                                    const DsRung* d_rungs, uint32_t num_rungs, uint32_t total_blocks,
+                                    float* out, uint64_t out_stride, uint32_t batch, hipStream_t s)
+{
+    if (!num_rungs || !total_blocks || !batch) return hipSuccess;
+    hipLaunchKernelGGL(downsample_ladder_kernel, dim3(total_blocks, batch), dim3(256), 0, s,
+                       x, n_in, x_stride, d_rungs, num_rungs, out, out_stride);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Cone kernel
+// ---------------------------------------------------------------------------
+// One workgroup = one ConeItem: `levels` merge levels of the FFA recursion for
+// the rows of one tile (or one whole node), held entirely in LDS.
+//
+//   level l (0 = target node, `levels` = deepest) is a packed list of row
+//   ranges, one per node of the split tree at that depth that the tile depends
+//   on.  Each merge step computes level l from level l+1 into registers
+//   (flattened over rows x phase bins, 34 values per thread), then overwrites
+//   the LDS level buffer.  The merge is transforms.hpp:13-27:
+//       out[u][j] = H[h(u)][j] + T[t(u)][(j + u - t(u)) mod p]
+//
+// LDS: 136 KiB level buffer + 8 KiB row descriptors + range tree = ~147 KiB,
+// i.e. one workgroup per CU.
+struct Range {          // rows [lo, hi] of one node of the split tree
+    int size;           // rows of the node
+    int lo, hi;         // node-local rows
+    int start;          // first row of the node within the transform
+    int base;           // first LDS row of this range in its level's packed layout
+    int child;          // index of the first child range (next level)
+};
+
+__device__ __forceinline__ int div_rows(int e, int p, float inv_p)
+{
+    int r = (int)((float)e * inv_p);
+    if (r * p > e) --r;
+    else if ((r + 1) * p <= e) ++r;
+    return r;
+}
+
+__device__ __forceinline__ double wave_incl_scan(double v, int lane)
+{
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double y = __shfl_up(v, o, 64);
+        if (lane >= o) v += y;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int wave_incl_scan_int(int v, int lane)
+{
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(v, o, 64);
+        if (lane >= o) v += y;
+    }
+    return v;
+}
+
+__device__ __forceinline__ float wave_max(float v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Index of the last range in [first, first+count) whose base <= r.
+__device__ __forceinline__ int find_range(const Range* ranges, int first, int count, int r)
+{
+    int lo = first, hi = first + count - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (ranges[mid].base <= r) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
+{
+    __shared__ float data[kLdsDataFloats];
+    __shared__ int2 desc[kMaxRows];
+    __shared__ Range ranges[kMaxRanges];
+    __shared__ int lv_first[kMaxTileLevels + 1];
+    __shared__ int lv_count[kMaxTileLevels + 1];
+    __shared__ int lv_rows[kMaxTileLevels + 1];
+
+    const ConeItem it = a.items[blockIdx.x];
+    const FfaXform X = a.xf[it.xform];
+    const int p = (int)X.p;
+    const float inv_p = 1.0f / (float)p;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int L = it.levels;
+    const bool tile = it.mode == kModeTile;
+    const uint64_t trial = blockIdx.y;
+
+    const float* src;
+    if (it.src == kSelLeaves) src = a.leaves + trial * a.leaves_stride + X.src_off;
+    else src = (it.src == kSelPing ? a.ping : a.pong) + trial * a.buf_stride + X.buf_off;
+
+    int nrows;
+    if (tile) {
+        // ---- dependency cone of the tile: top-down range tree, one lane per range (wave 0)
+        if (wave == 0) {
+            if (lane == 0) {
+                Range r0;
+                r0.size = (int)it.node_size;
+                r0.lo = (int)it.s0;
+                r0.hi = (int)it.s1 - 1;
+                r0.start = (int)it.node_start;
+                r0.base = 0;
+                r0.child = 0;
+                ranges[0] = r0;
+                lv_first[0] = 0;
+                lv_count[0] = 1;
+                lv_rows[0] = r0.hi - r0.lo + 1;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            int first = 0, count = 1;
+            for (int l = 0; l < L; ++l) {
+                const int nfirst = first + count;
+                Range r, h, t;
+                int nchild = 0, c0 = 0, c1 = 0;
+                if (lane < count) {
+                    r = ranges[first + lane];
+                    if (r.size <= 1) {          // a leaf is carried unchanged
+                        nchild = 1;
+                        h = r;
+                        c0 = r.hi - r.lo + 1;
+                    } else {
+                        nchild = 2;
+                        const int sh = r.size >> 1, st = r.size - sh;
+                        const float kh = merge_coef((uint32_t)sh, (uint32_t)r.size);
+                        const float kt = merge_coef((uint32_t)st, (uint32_t)r.size);
+                        h.size = sh;
+                        h.lo = (int)merge_index(kh, (uint32_t)r.lo);
+                        h.hi = (int)merge_index(kh, (uint32_t)r.hi);
+                        h.start = r.start;
+                        t.size = st;
+                        t.lo = (int)merge_index(kt, (uint32_t)r.lo);
+                        t.hi = (int)merge_index(kt, (uint32_t)r.hi);
+                        t.start = r.start + sh;
+                        c0 = h.hi - h.lo + 1;
+                        c1 = t.hi - t.lo + 1;
+                    }
+                }
+                const int pos_incl = wave_incl_scan_int(nchild, lane);
+                const int rows_incl = wave_incl_scan_int(c0 + c1, lane);
+                const int total = __shfl(pos_incl, 63, 64);
+                const int total_rows = __shfl(rows_incl, 63, 64);
+                if (lane < count) {
+                    const int pos = nfirst + pos_incl - nchild;
+                    const int rbase = rows_incl - (c0 + c1);
+                    h.base = rbase;
+                    h.child = 0;
+                    ranges[pos] = h;
+                    if (nchild == 2) {
+                        t.base = rbase + c0;
+                        t.child = 0;
+                        ranges[pos + 1] = t;
+                    }
+                    ranges[first + lane].child = pos;
+                }
+                if (lane == 0) {
+                    lv_first[l + 1] = nfirst;
+                    lv_count[l + 1] = total;
+                    lv_rows[l + 1] = total_rows;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                first = nfirst;
+                count = total;
+            }
+        }
+        __syncthreads();
+        nrows = lv_rows[L];
+        if (nrows > kMaxRows || nrows * p > kLdsDataFloats) {
+            if (tid == 0 && a.error_flag) atomicOr(a.error_flag, 1);
+            return;
+        }
+        // ---- bottom level: source row of every LDS row, then the load
+        const int bf = lv_first[L], bc = lv_count[L];
+        for (int r = tid; r < nrows; r += kConeBlock) {
+            const Range R = ranges[find_range(ranges, bf, bc, r)];
+            desc[r].x = R.start + R.lo + (r - R.base);
+        }
+        __syncthreads();
+        const int total = nrows * p;
+        for (int e = tid; e < total; e += kConeBlock) {
+            const int r = div_rows(e, p, inv_p);
+            const int col = e - r * p;
+            data[e] = src[(uint64_t)desc[r].x * p + col];
+        }
+    } else {
+        nrows = (int)it.node_size;
+        if (nrows > kMaxRows || nrows * p > kLdsDataFloats) {
+            if (tid == 0 && a.error_flag) atomicOr(a.error_flag, 2);
+            return;
+        }
+        const float* s = src + (uint64_t)it.node_start * p;
+        const int total = nrows * p;
+        for (int e = tid; e < total; e += kConeBlock) data[e] = s[e];
+    }
+    __syncthreads();
+
+    // ---- merge levels, deepest first
+    for (int l = L - 1; l >= 0; --l) {
+        const int orows = tile ? lv_rows[l] : (int)it.node_size;
+        for (int r = tid; r < orows; r += kConeBlock) {
+            int hrow, trow = -1, shift = 0;
+            if (tile) {
+                const Range R = ranges[find_range(ranges, lv_first[l], lv_count[l], r)];
+                const int u = R.lo + (r - R.base);
+                const Range H = ranges[R.child];
+                if (R.size <= 1) {
+                    hrow = H.base + (u - H.lo);
+                } else {
+                    const Range T = ranges[R.child + 1];
+                    const int sh = R.size >> 1, st = R.size - sh;
+                    const int h = (int)merge_index(merge_coef((uint32_t)sh, (uint32_t)R.size), (uint32_t)u);
+                    const int t = (int)merge_index(merge_coef((uint32_t)st, (uint32_t)R.size), (uint32_t)u);
+                    hrow = H.base + (h - H.lo);
+                    trow = T.base + (t - T.lo);
+                    shift = (u - t) % p;
+                }
+            } else {
+                int a0 = 0, sz = (int)it.node_size;
+                for (int d = 0; d < l; ++d) {
+                    if (sz > 1) {
+                        const int hs = sz >> 1;
+                        if (r - a0 < hs) sz = hs;
+                        else { a0 += hs; sz -= hs; }
+                    }
+                }
+                if (sz <= 1) {
+                    hrow = r;
+                } else {
+                    const int s = r - a0;
+                    const int sh = sz >> 1, st = sz - sh;
+                    const int h = (int)merge_index(merge_coef((uint32_t)sh, (uint32_t)sz), (uint32_t)s);
+                    const int t = (int)merge_index(merge_coef((uint32_t)st, (uint32_t)sz), (uint32_t)s);
+                    hrow = a0 + h;
+                    trow = a0 + sh + t;
+                    shift = (s - t) % p;
+                }
+            }
+            const int ho = hrow * p;
+            const int to = trow < 0 ? 0xFFFF : trow * p;
+            desc[r] = make_int2(ho | (to << 16), shift);
+        }
+        __syncthreads();
+        const int total = orows * p;
+        float v[kRegsPerThread];
+        // (row, col) of element e = k * kConeBlock + tid, advanced incrementally
+        int r = div_rows(tid, p, inv_p);
+        int col = tid - r * p;
+        int rem = total - tid;
+        // opaque per level: stops LICM from hoisting all per-element indices
+        // out of the level loop (which spills the register file)
+        asm volatile("" : "+v"(r), "+v"(col), "+v"(rem));
+        const int dr = kConeBlock / p, dc = kConeBlock - (kConeBlock / p) * p;
+#pragma unroll
+        for (int k = 0; k < kRegsPerThread; ++k) {
+            if (rem > k * kConeBlock) {
+                const int2 d = desc[r];
+                const int ho = d.x & 0xFFFF;
+                const int to = (int)((unsigned)d.x >> 16);
+                float x = data[ho + col];
+                if (to != 0xFFFF) {
+                    int c2 = col + d.y;
+                    if (c2 >= p) c2 -= p;
+                    x = __fadd_rn(x, data[to + c2]);
+                }
+                v[k] = x;
+            }
+            r += dr;
+            col += dc;
+            if (col >= p) {
+                col -= p;
+                ++r;
+            }
+            // bound the live ranges: at most 4 elements' loads in flight per thread
+            if ((k & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kRegsPerThread; ++k) {
+            const int e = k * kConeBlock + tid;
+            if (e < total) data[e] = v[k];
+        }
+        __syncthreads();
+        nrows = orows;
+    }
+
+    // ---- output: tile rows [s0, s0 + nrows) of the node
+    if (it.dst != kSelSnr) {
+        float* dst = (it.dst == kSelPing ? a.ping : a.pong) + trial * a.buf_stride + X.buf_off +
+                     (uint64_t)(it.node_start + it.s0) * p;
+        const int total = nrows * p;
+        for (int e = tid; e < total; e += kConeBlock) dst[e] = data[e];
+        return;
+    }
+
+    // ---- fused boxcar S/N epilogue (snr.hpp:37-65) on the root's rows s < rows_eval
+    const int nev = (int)min((int64_t)nrows, (int64_t)X.rows_eval - (int64_t)it.s0);
+    if (nev <= 0) return;
+    const int c = (p + 63) >> 6;
+    const int j0 = min(lane * c, p);
+    const int j1 = min(j0 + c, p);
+    const int owner = (p - 1) / c;
+    for (int r = wave; r < nev; r += kConeBlock / 64) {
+        float* row = data + r * p;
+        double part = 0.0;
+        for (int j = j0; j < j1; ++j) part += (double)row[j];
+        const double incl = wave_incl_scan(part, lane);
+        double acc = __shfl_up(incl, 1, 64);
+        if (lane == 0) acc = 0.0;
+        for (int j = j0; j < j1; ++j) {
+            acc += (double)row[j];
+            row[j] = (float)acc;    // circular_prefix_sum, kernels.hpp:73-86 (fp64 accumulator)
+        }
+        const float sum = __shfl((float)acc, owner, 64);
+        if (lane == 0) desc[r].x = __float_as_int(sum);
+    }
+    __syncthreads();
+    const uint32_t nw = a.num_widths;
+    float* snr = a.snr + trial * a.snr_stride + (X.snr_row + it.s0) * (uint64_t)nw;
+    for (int r = wave; r < nev; r += kConeBlock / 64) {
+        const float* row = data + r * p;
+        const float sum = __int_as_float(desc[r].x);
+        for (uint32_t iw = 0; iw < nw; ++iw) {
+            const int w = (int)a.widths[iw];
+            float dmax = -INFINITY;
+            for (int i = j0; i < j1; ++i) {
+                const int k = i + w;
+                const float ck = k < p ? row[k] : __fadd_rn(row[k - p], sum);
+                dmax = fmaxf(dmax, __fsub_rn(ck, row[i]));
+            }
+            dmax = wave_max(dmax);
+            if (lane == 0) {
+                const float h = sqrtf((float)(p - w) / (float)(p * w));
+                const float b = (float)w / (float)(p - w) * h;
+                snr[(uint64_t)r * nw + iw] = ((h + b) * dmax - b * sum) / X.stdnoise;
+            }
+        }
+    }
+}
+
+hipError_t launch_cone(const ConeArgs& args, uint32_t batch, hipStream_t s)
+{
+    if (!args.num_items || !batch) return hipSuccess;
+    hipLaunchKernelGGL(cone_kernel, dim3(args.num_items, batch), dim3(kConeBlock), 0, s, args);
+    return hipGetLastError();
+}
+
+}  // namespace rt
+
+namespace rt {
+
+// ---------------------------------------------------------------------------
+// Fallback for rows too wide for the LDS cone kernel (ffa2 with p > ~11k):
+// one launch per tree depth, one workgroup per output row, global memory.
+// nodes[] = (start, size) of every node at this depth, sorted by start.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void ffa_level_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                        const uint2* __restrict__ nodes, uint32_t num_nodes,
+                                                        uint32_t p)
+{
+    const uint32_t u = blockIdx.x;
+    uint32_t lo = 0, hi = num_nodes - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (nodes[mid].x <= u) lo = mid; else hi = mid - 1;
+    }
+    const uint2 nd = nodes[lo];
+    const float* hrow;
+    const float* trow = nullptr;
+    uint32_t shift = 0;
+    if (nd.y <= 1) {
+        hrow = in + (uint64_t)u * p;
+    } else {
+        const uint32_t s = u - nd.x, sh = nd.y >> 1, st = nd.y - sh;
+        const uint32_t h = merge_index(merge_coef(sh, nd.y), s);
+        const uint32_t t = merge_index(merge_coef(st, nd.y), s);
+        hrow = in + (uint64_t)(nd.x + h) * p;
+        trow = in + (uint64_t)(nd.x + sh + t) * p;
+        shift = (s - t) % p;
+    }
+    float* o = out + (uint64_t)u * p;
+    for (uint32_t j = threadIdx.x; j < p; j += 256) {
+        float v = hrow[j];
+        if (trow) {
+            uint32_t c = j + shift;
+            if (c >= p) c -= p;
+            v = __fadd_rn(v, trow[c]);
+        }
+        o[j] = v;
+    }
+}
+
+hipError_t launch_ffa_level(const float* in, float* out, const uint2* d_nodes, uint32_t num_nodes,
+                            uint32_t rows, uint32_t p, hipStream_t s)
+{
+    hipLaunchKernelGGL(ffa_level_kernel, dim3(rows), dim3(256), 0, s, in, out, d_nodes, num_nodes, p);
+    return hipGetLastError();
+}
+
+}  // namespace rt

@@ -1,0 +1,42 @@
+// Launch wrappers of the HIP kernels (host-callable, stream-ordered, no sync).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+
+namespace rt {
+
+struct DsRung {
+    double f;
+    uint64_t n;          // output samples of this rung
+    uint64_t out_off;    // float offset in the per-trial leaf buffer
+    uint32_t first_block;
+    uint32_t identity;   // f == 1: plain copy
+};
+
+// ffa_kernels.hip
+hipError_t launch_downsample_ladder(const float* x, uint64_t n_in, uint64_t x_stride,
+                                    const DsRung* d_rungs, uint32_t num_rungs, uint32_t total_blocks,
+                                    float* out, uint64_t out_stride, uint32_t batch, hipStream_t s);
+hipError_t launch_cone(const ConeArgs& args, uint32_t batch, hipStream_t s);
+hipError_t launch_ffa_level(const float* in, float* out, const uint2* d_nodes, uint32_t num_nodes,
+                            uint32_t rows, uint32_t p, hipStream_t s);
+
+// aux_kernels.hip
+hipError_t launch_snr_rows(const float* x, uint64_t rows, uint32_t cols, const uint32_t* d_widths,
+                           uint32_t nw, float stdnoise, float* cps_scratch, float* out, hipStream_t s);
+hipError_t launch_running_median(const float* x, uint64_t n, uint32_t width, float* out, uint64_t x_stride,
+                                 uint64_t out_stride, uint32_t batch, hipStream_t s);
+hipError_t launch_scrunch(const float* x, uint64_t n_out, uint32_t factor, float* out, uint64_t x_stride,
+                          uint64_t out_stride, uint32_t batch, hipStream_t s);
+hipError_t launch_deredden_subtract(const float* x, uint64_t n, const float* rmed_lo, uint64_t n_lo,
+                                    uint32_t factor, float* out, uint64_t x_stride, uint64_t lo_stride,
+                                    uint64_t out_stride, uint32_t batch, hipStream_t s);
+hipError_t launch_interp(uint64_t n, const float* rmed_lo, uint64_t n_lo, uint32_t factor, double* out,
+                         hipStream_t s);
+hipError_t launch_normalise(const float* x, uint64_t n, float* out, double* d_partials, uint32_t nblocks,
+                            uint64_t x_stride, uint64_t out_stride, uint32_t batch, hipStream_t s);
+hipError_t launch_rollback(const float* x, uint64_t n, uint64_t shift, const float* y, float* out, hipStream_t s);
+hipError_t launch_circular_prefix_sum(const float* x, uint64_t n, uint64_t nsum, float* out, hipStream_t s);
+
+}  // namespace rt

@@ -1,0 +1,310 @@
+// Host planner.  Compiled with -ffp-contract=off -mfma: every floating-point
+// expression is evaluated as written, and the one FMA the reference binary
+// emits (the period grid) is requested explicitly.
+#include "plan.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <stdexcept>
+
+namespace rt {
+
+std::string check_pgram_args(const PgramParams& a)
+{
+    // periodogram.hpp:25-40 (same order, same messages)
+    if (!(a.tsamp > 0)) return "tsamp must be > 0";
+    if (!(a.pmin > 0)) return "period_min must be > 0";
+    if (!(a.pmax > a.pmin)) return "period_max must be > period_min";
+    if (!(a.bmin > 1)) return "bins_min must be > 1";
+    if (!(a.bmax >= a.bmin)) return "bins_max must be >= bins_min";
+    if (!(a.pmin >= a.tsamp * (double)a.bmin)) return "Must have: period_min >= tsamp * bins_min ";
+    return "";
+}
+
+size_t downsampled_size(size_t n, double f)
+{
+    return (size_t)std::floor((double)n / f);
+}
+
+double downsampled_variance(size_t n, double f)
+{
+    const double k = std::floor(f);
+    const double r = f - k;
+    const double x = (double)downsampled_size(n, f) * r;
+    if (x > 1.0) return f - 1.0 / 3.0;
+    return (k - 1.0) * (k - 1.0) + 2.0 / 3.0 * (x * x) - x + 1.0;
+}
+
+static size_t ceilshift(size_t rows, size_t cols, double pmax)
+{
+    // periodogram.hpp:54-57
+    return (size_t)std::ceil((double)cols * ((double)rows - 1.0) * (1.0 - (double)cols / pmax));
+}
+
+void build_pgram_plan(const PgramParams& a, PgramPlan& plan)
+{
+    plan = PgramPlan();
+    plan.prm = a;
+    const double ds_ini = a.pmin / (a.tsamp * (double)a.bmin);
+    const double ds_geo = ((double)a.bmax + 1.0) / (double)a.bmin;
+    const size_t nds = (size_t)std::ceil(std::log(a.pmax / a.pmin) / std::log(ds_geo));
+    uint64_t leaf = 0, row = 0;
+    for (size_t ids = 0; ids < nds; ++ids) {
+        Rung r;
+        r.f = ds_ini * std::pow(ds_geo, (double)ids);
+        r.tau = r.f * a.tsamp;
+        r.n = downsampled_size(a.size, r.f);
+        r.leaf_off = leaf;
+        const double pmax_samples = a.pmax / r.tau;
+        size_t bstop = std::min(a.bmax, r.n);
+        bstop = std::min(bstop, (size_t)pmax_samples);
+        const uint32_t rung_index = (uint32_t)plan.rungs.size();
+        bool used = false;
+        for (size_t bins = a.bmin; bins <= bstop; ++bins) {
+            Step s;
+            s.rung = rung_index;
+            s.bins = (uint32_t)bins;
+            s.rows = (uint32_t)(r.n / bins);
+            s.stdnoise = (float)std::sqrt((double)s.rows * downsampled_variance(a.size, r.f));
+            const double pceil = std::min(pmax_samples, (double)bins + 1.0);
+            s.rows_eval = (uint32_t)std::min((size_t)s.rows, ceilshift(s.rows, bins, pceil));
+            s.out_row = row;
+            row += s.rows_eval;
+            plan.steps.push_back(s);
+            used = true;
+        }
+        plan.rungs.push_back(r);
+        if (used) leaf += (r.n + 3) & ~(uint64_t)3;   // 16-byte aligned rungs
+    }
+    plan.length = row;
+    plan.leaf_floats = leaf;
+}
+
+void fill_grid(const PgramPlan& plan, double* periods, uint32_t* foldbins)
+{
+    for (const Step& s : plan.steps) {
+        const double tau = plan.rungs[s.rung].tau;
+        const uint64_t B = s.bins;
+        const double num = (double)(B * B) * tau;
+        const double r = -1.0 / ((double)s.rows - 1.0);
+        for (uint32_t i = 0; i < s.rows_eval; ++i) {
+            periods[s.out_row + i] = num / std::fma((double)i, r, (double)B);
+            foldbins[s.out_row + i] = (uint32_t)B;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Pass schedule
+// ---------------------------------------------------------------------------
+static int ceil_log2(uint32_t s)
+{
+    int l = 0;
+    while ((1u << l) < s) ++l;
+    return l;
+}
+
+struct Node { uint32_t start, size; };
+
+static void nodes_at_depth(uint32_t m, int depth, std::vector<Node>& out)
+{
+    out.clear();
+    out.push_back({0, m});
+    for (int d = 0; d < depth; ++d) {
+        std::vector<Node> nxt;
+        nxt.reserve(out.size() * 2);
+        for (const Node& n : out) {
+            if (n.size <= 1) { nxt.push_back(n); continue; }
+            const uint32_t h = n.size >> 1;
+            nxt.push_back({n.start, h});
+            nxt.push_back({n.start + h, n.size - h});
+        }
+        out.swap(nxt);
+    }
+}
+
+ConeNeed cone_need(uint32_t node_size, uint32_t s0, uint32_t s1, int levels, uint32_t p)
+{
+    struct R { uint32_t size, lo, hi; };
+    std::vector<R> cur{{node_size, s0, s1 - 1}}, nxt;
+    ConeNeed need;
+    auto account = [&](const std::vector<R>& lv) {
+        int rows = 0, floats = 0;
+        for (const R& r : lv) {
+            rows += (int)(r.hi - r.lo + 1);
+            floats += (int)((r.hi - r.lo + 1) * p + 3);
+        }
+        need.max_rows = std::max(need.max_rows, rows);
+        need.max_floats = std::max(need.max_floats, floats);
+        need.ranges += (int)lv.size();
+    };
+    account(cur);
+    for (int l = 0; l < levels; ++l) {
+        nxt.clear();
+        for (const R& r : cur) {
+            if (r.size <= 1) { nxt.push_back(r); continue; }
+            const uint32_t sh = r.size >> 1, st = r.size - sh;
+            const float kh = merge_coef(sh, r.size), kt = merge_coef(st, r.size);
+            nxt.push_back({sh, merge_index(kh, r.lo), merge_index(kh, r.hi)});
+            nxt.push_back({st, merge_index(kt, r.lo), merge_index(kt, r.hi)});
+        }
+        cur.swap(nxt);
+        account(cur);
+    }
+    return need;
+}
+
+static bool fits(const ConeNeed& n)
+{
+    return n.max_rows <= kMaxRows && n.max_floats <= kLdsDataFloats && n.ranges <= kMaxRanges;
+}
+
+// Per-transform schedule: list of passes, each a list of (node, tile, levels).
+struct PassItems { std::vector<ConeItem> items; double read = 0, written = 0; };
+
+static void plan_transform(const FfaXform& X, uint32_t xi, std::vector<PassItems>& passes)
+{
+    passes.clear();
+    const uint32_t m = X.m, p = X.p;
+    const int C = lds_row_capacity(p);
+    if (C < 3) throw std::invalid_argument("phase bins too large for the LDS cone kernel");
+    // bottom depth: every node at depth db transforms whole in LDS
+    int db = 0;
+    while (((uint64_t)m + (1ull << db) - 1) >> db > (uint64_t)C) ++db;
+    std::vector<Node> nodes;
+    nodes_at_depth(m, db, nodes);
+    PassItems bottom;
+    for (const Node& n : nodes) {
+        ConeItem it{};
+        it.xform = xi;
+        it.node_start = n.start;
+        it.node_size = n.size;
+        it.s0 = 0;
+        it.s1 = n.size;
+        it.levels = (uint8_t)ceil_log2(n.size);
+        it.mode = kModeWhole;
+        bottom.items.push_back(it);
+        bottom.read += 4.0 * n.size * p;
+        bottom.written += 4.0 * n.size * p;
+    }
+    passes.push_back(std::move(bottom));
+    if (db == 0) return;
+
+    // upper levels: db merge levels in passes of L (cost model: cone overhead vs passes)
+    int bestL = 1;
+    double best = 1e300;
+    for (int L = 1; L <= kMaxTileLevels; ++L) {
+        const int extra = 2 << L;
+        if (extra + 1 >= C) break;
+        const int npass = (db + L - 1) / L;
+        const double cost = npass * ((double)C / (double)(C - extra) + 1.0);
+        if (cost < best - 1e-9) { best = cost; bestL = L; }
+    }
+    const int npass = (db + bestL - 1) / bestL;
+    // split db levels as evenly as possible; deeper passes first
+    std::vector<int> lv(npass, db / npass);
+    for (int i = 0; i < db % npass; ++i) lv[i] += 1;
+    int depth_below = db;   // depth whose rows the next pass reads
+    for (int k = 0; k < npass; ++k) {
+        const int L = lv[k];
+        const int dtop = depth_below - L;
+        nodes_at_depth(m, dtop, nodes);
+        PassItems pass;
+        const int guess = std::max(1, C - (2 << L) - 2);
+        for (const Node& n : nodes) {
+            uint32_t s0 = 0;
+            while (s0 < n.size) {
+                uint32_t K = std::min<uint32_t>((uint32_t)guess, n.size - s0);
+                ConeNeed need = cone_need(n.size, s0, s0 + K, L, p);
+                while (K > 1 && !fits(need)) {
+                    K -= std::max<uint32_t>(1, K / 32);
+                    need = cone_need(n.size, s0, s0 + K, L, p);
+                }
+                if (!fits(need)) throw std::invalid_argument("cone tile does not fit in LDS");
+                while (s0 + K < n.size) {
+                    ConeNeed nn = cone_need(n.size, s0, s0 + K + 1, L, p);
+                    if (!fits(nn)) break;
+                    need = nn;
+                    ++K;
+                }
+                ConeItem it{};
+                it.xform = xi;
+                it.node_start = n.start;
+                it.node_size = n.size;
+                it.s0 = s0;
+                it.s1 = s0 + K;
+                it.levels = (uint8_t)L;
+                it.mode = kModeTile;
+                pass.items.push_back(it);
+                // rows read at the cone bottom (upper bound: max level) + rows written
+                pass.read += 4.0 * need.max_rows * p;
+                pass.written += 4.0 * K * p;
+                s0 += K;
+            }
+        }
+        passes.push_back(std::move(pass));
+        depth_below = dtop;
+    }
+}
+
+void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uint32_t num_widths,
+                     uint64_t scratch_budget, ExecPlan& out)
+{
+    out = ExecPlan();
+    out.xf = xforms;
+    const size_t nx = xforms.size();
+    size_t g0 = 0;
+    uint32_t group = 0;
+    std::vector<std::vector<PassItems>> sched;
+    while (g0 < nx) {
+        // group [g0, g1): scratch fits the budget (always at least one transform)
+        uint64_t scratch = 0;
+        size_t g1 = g0;
+        while (g1 < nx) {
+            const uint64_t cells = ((uint64_t)xforms[g1].m * xforms[g1].p + 3) & ~(uint64_t)3;
+            if (g1 > g0 && scratch + cells > scratch_budget) break;
+            out.xf[g1].buf_off = scratch;
+            scratch += cells;
+            ++g1;
+        }
+        out.scratch_floats = std::max(out.scratch_floats, scratch);
+        sched.assign(g1 - g0, {});
+        uint32_t gpasses = 0;
+        for (size_t i = g0; i < g1; ++i) {
+            plan_transform(out.xf[i], (uint32_t)i, sched[i - g0]);
+            gpasses = std::max<uint32_t>(gpasses, (uint32_t)sched[i - g0].size());
+        }
+        out.max_passes = std::max(out.max_passes, gpasses);
+        for (uint32_t k = 0; k < gpasses; ++k) {
+            Launch L;
+            L.first = (uint32_t)out.items.size();
+            L.group = group;
+            L.pass = k;
+            for (size_t i = g0; i < g1; ++i) {
+                auto& sp = sched[i - g0];
+                const uint32_t P = (uint32_t)sp.size();
+                if (k >= P) continue;
+                const FfaXform& X = out.xf[i];
+                const uint8_t src = k == 0 ? kSelLeaves : (((P - k) % 2 == 0) ? kSelPing : kSelPong);
+                const bool last = (k == P - 1);
+                const uint8_t dst = last ? (snr_epilogue ? kSelSnr : kSelPing)
+                                         : (((P - 1 - k) % 2 == 0) ? kSelPing : kSelPong);
+                for (ConeItem it : sp[k].items) {
+                    it.src = src;
+                    it.dst = dst;
+                    out.items.push_back(it);
+                }
+                const double cells = (double)X.m * X.p;
+                L.cells += (uint64_t)X.m * X.p;
+                L.alg_bytes += 4.0 * cells + ((last && snr_epilogue) ? 4.0 * X.rows_eval * num_widths : 4.0 * cells);
+                L.moved_bytes += sp[k].read + ((last && snr_epilogue) ? 4.0 * X.rows_eval * num_widths : sp[k].written);
+            }
+            L.count = (uint32_t)out.items.size() - L.first;
+            if (L.count) out.launches.push_back(L);
+        }
+        g0 = g1;
+        ++group;
+    }
+}
+
+}  // namespace rt

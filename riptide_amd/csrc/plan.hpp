@@ -1,0 +1,79 @@
+// Host-side planner: periodogram ladder (bit-exact with periodogram.hpp), the
+// trial-period grid, and the pass / work-item schedule of the cone kernel.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+
+namespace rt {
+
+struct PgramParams {
+    size_t size = 0;       // input samples N
+    double tsamp = 0, pmin = 0, pmax = 0;
+    size_t bmin = 0, bmax = 0;
+};
+
+// periodogram.hpp:25-40.  Returns the reference's exception text, or "" if valid.
+std::string check_pgram_args(const PgramParams& a);
+
+// downsample.hpp:11-38
+size_t downsampled_size(size_t n, double f);
+double downsampled_variance(size_t n, double f);
+
+struct Rung {
+    double f = 0, tau = 0;
+    size_t n = 0;          // downsampled length
+    uint64_t leaf_off = 0; // float offset in the per-trial leaf buffer
+};
+
+struct Step {              // one (rung, bins) FFA transform
+    uint32_t rung = 0, bins = 0, rows = 0, rows_eval = 0;
+    float stdnoise = 0;
+    uint64_t out_row = 0;  // first grid/S/N row
+};
+
+struct PgramPlan {
+    PgramParams prm;
+    std::vector<Rung> rungs;
+    std::vector<Step> steps;
+    uint64_t length = 0;       // periodogram_length (periodogram.hpp:63-109)
+    uint64_t leaf_floats = 0;  // per-trial leaf buffer (all rungs)
+};
+
+// Ladder + steps (periodogram.hpp:135-183).  Arguments must be valid.
+void build_pgram_plan(const PgramParams& a, PgramPlan& plan);
+
+// periods[s] / foldbins[s] for all L rows (periodogram.hpp:260-264, in the form
+// the reference binary evaluates it: (B*B*tau) / fma(s, -1/(rows-1), B)).
+void fill_grid(const PgramPlan& plan, double* periods, uint32_t* foldbins);
+
+struct Launch {
+    uint32_t first = 0, count = 0;   // item range
+    uint32_t group = 0, pass = 0;
+    double alg_bytes = 0;            // 4mp read + (4mp | 4*rows_eval*W) write
+    double moved_bytes = 0;          // bytes the items actually read + write (cone overlap incl.)
+    uint64_t cells = 0;              // sum m*p of the transforms in this launch
+};
+
+struct ExecPlan {
+    std::vector<FfaXform> xf;
+    std::vector<ConeItem> items;
+    std::vector<Launch> launches;
+    uint64_t scratch_floats = 0;     // per ping/pong buffer, per trial
+    uint32_t max_passes = 0;
+};
+
+// Schedule a list of transforms (p, m, rows_eval, src_off, snr_row, stdnoise
+// filled in by the caller).  With snr_epilogue the last pass of every
+// transform writes S/N rows; otherwise it writes the transform into `ping`.
+// Transforms are grouped so that each group's scratch fits scratch_budget
+// floats per buffer; a group's passes are consecutive launches.
+void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uint32_t num_widths,
+                     uint64_t scratch_budget, ExecPlan& out);
+
+// Dependency-cone footprint of one tile (host mirror of the device range tree).
+struct ConeNeed { int max_rows = 0; int max_floats = 0; int ranges = 0; };
+ConeNeed cone_need(uint32_t node_size, uint32_t s0, uint32_t s1, int levels, uint32_t p);
+
+}  // namespace rt

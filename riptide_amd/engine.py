@@ -1,0 +1,145 @@
+"""Device-resident, batched hot path (the part bench.py and the multi-GPU
+dispatcher drive).  Buffers are torch tensors on the ROCm device; all compute
+is the engine's HIP kernels (rt_plan_* / rt_periodogram_device /
+rt_deredden_normalise_device in include/riptide_amd.h).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .ffautils import generate_width_trials
+
+_L = _lib.load()
+_check = _lib.check
+
+
+def _stream_handle(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class PeriodogramPlan:
+    """Compiled periodogram plan for series of `size` samples: downsampling
+    ladder, trial grid and the cone-kernel pass schedule (host-built once,
+    uploaded to the current device)."""
+
+    def __init__(self, size, tsamp, widths, period_min, period_max, bins_min, bins_max, device=None):
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        _check(_L.rt_set_device(dev.index))
+        self.device = dev
+        self.size, self.tsamp = int(size), float(tsamp)
+        self.widths = np.ascontiguousarray(widths, dtype=np.uint64)
+        self.period_min, self.period_max = float(period_min), float(period_max)
+        self.bins_min, self.bins_max = int(bins_min), int(bins_max)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            _check(_L.rt_plan_create(self.size, self.tsamp, _lib.ptr(self.widths), self.widths.size,
+                                     self.period_min, self.period_max, self.bins_min, self.bins_max,
+                                     ctypes.byref(h)))
+        self._h = h
+        L, W = ctypes.c_size_t(), ctypes.c_size_t()
+        _check(_L.rt_plan_shape(h, ctypes.byref(L), ctypes.byref(W)))
+        self.length, self.num_widths = L.value, W.value
+        self._grid = None
+
+    @classmethod
+    def for_search(cls, size, tsamp, period_min, period_max, bins_min=240, bins_max=260, ducy_max=0.2,
+                   wtsp=1.5, device=None):
+        widths = generate_width_trials(bins_min, ducy_max=ducy_max, wtsp=wtsp)
+        return cls(size, tsamp, widths, period_min, period_max, bins_min, bins_max, device=device)
+
+    def grid(self):
+        """(periods f64[L], foldbins u32[L]) -- bit-exact with the reference."""
+        if self._grid is None:
+            periods = np.empty(self.length, dtype=np.float64)
+            foldbins = np.empty(self.length, dtype=np.uint32)
+            _check(_L.rt_plan_grid(self._h, _lib.ptr(periods), _lib.ptr(foldbins)))
+            self._grid = (periods, foldbins)
+        return self._grid
+
+    def workspace_bytes(self, batch):
+        b = ctypes.c_size_t()
+        _check(_L.rt_plan_workspace_bytes(self._h, int(batch), ctypes.byref(b)))
+        return b.value
+
+    def stats(self):
+        u = [ctypes.c_uint64() for _ in range(4)]
+        d = [ctypes.c_double() for _ in range(2)]
+        _check(_L.rt_plan_stats(self._h, *(ctypes.byref(x) for x in u[:3]), ctypes.byref(d[0]),
+                                ctypes.byref(d[1]), ctypes.byref(u[3])))
+        return {"transforms": u[0].value, "items": u[1].value, "launches": u[2].value,
+                "alg_bytes": d[0].value, "moved_bytes": d[1].value, "cells": u[3].value}
+
+    def run(self, data, out=None, workspace=None, stream=None):
+        """S/N of a batch of series: data float32 [B, size] (or [size]) on the
+        device -> float32 [B, L, W].  Stream-ordered; no host synchronisation."""
+        import torch
+        squeeze = data.dim() == 1
+        if squeeze:
+            data = data.unsqueeze(0)
+        if data.dtype != torch.float32 or data.device != self.device or data.shape[1] != self.size:
+            raise ValueError("data must be float32 [B, size] on the plan's device")
+        if data.stride(1) != 1:
+            raise ValueError("data rows must be contiguous")
+        B = data.shape[0]
+        if out is None:
+            out = torch.empty((B, self.length, self.num_widths), dtype=torch.float32, device=self.device)
+        need = self.workspace_bytes(B)
+        if workspace is None or workspace.numel() < need:
+            workspace = torch.empty(need, dtype=torch.uint8, device=self.device)
+        _check(_L.rt_periodogram_device(self._h, _lib.ptr(data), B, data.stride(0), _lib.ptr(out),
+                                        self.length * self.num_widths, _lib.ptr(workspace), workspace.numel(),
+                                        _stream_handle(stream)))
+        return out[0] if squeeze else out
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            _L.rt_plan_destroy(h)
+            self._h = None
+
+
+def deredden_workspace_bytes(size, width_samples, min_points, batch):
+    b = ctypes.c_size_t()
+    _check(_L.rt_deredden_workspace_bytes(int(size), int(width_samples), int(min_points), int(batch),
+                                          ctypes.byref(b)))
+    return b.value
+
+
+def deredden_normalise(data, width_samples, min_points=101, deredden=True, normalise=True, out=None,
+                       workspace=None, stream=None):
+    """TimeSeries.deredden(...).normalise() for a batch [B, N] of device series."""
+    import torch
+    squeeze = data.dim() == 1
+    if squeeze:
+        data = data.unsqueeze(0)
+    B, N = data.shape
+    if out is None:
+        out = torch.empty_like(data)
+    need = deredden_workspace_bytes(N, width_samples, min_points, B)
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=data.device)
+    _check(_L.rt_deredden_normalise_device(_lib.ptr(data), N, B, data.stride(0), int(width_samples),
+                                           int(min_points), int(bool(deredden)), int(bool(normalise)),
+                                           _lib.ptr(out), out.stride(0), _lib.ptr(workspace), workspace.numel(),
+                                           _stream_handle(stream)))
+    return out[0] if squeeze else out
+
+
+def profile_enable(on=True):
+    _check(_L.rt_profile_enable(int(bool(on))))
+
+
+def profile_reset():
+    _check(_L.rt_profile_reset())
+
+
+def profile_read(kind=0):
+    """Accumulated (ms, algorithmic bytes, moved bytes, launches) of the cone
+    kernel (kind 0) or the downsample ladder (kind 1) since the last reset."""
+    ms, alg, mv, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
+    _check(_L.rt_profile_read(int(kind), ctypes.byref(ms), ctypes.byref(alg), ctypes.byref(mv), ctypes.byref(n)))
+    return {"ms": ms.value, "alg_bytes": alg.value, "moved_bytes": mv.value, "launches": n.value}

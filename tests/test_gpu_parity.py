@@ -1,0 +1,289 @@
+"""Parity of the HIP path (through the C ABI) with the oracle and the golden
+vectors of the reference.  Bit-exact: FFA transform, downsample (vs the strict
+oracle), trial grid, running median, dereddened series.  S/N: 1e-4 relative
+(BASELINE.json), scaled by max(|ref|, 1) since S/N is in units of sigma.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+import inputs
+from conftest import snr_close
+
+pytestmark = pytest.mark.gpu
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def rt():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm device")
+    import riptide_amd
+    return riptide_amd
+
+
+# ---------------------------------------------------------------- FFA transform
+def test_ffa_known_answer(rt):
+    # test_ffa_base_functions.py:35-56
+    for shift in range(8):
+        x = np.roll(inputs.FFA_IN_88, shift, axis=1)
+        truth = np.roll(inputs.FFA_OUT_88, shift, axis=1)
+        assert np.array_equal(rt.ffa2(x), truth)
+        assert np.array_equal(rt.ffa1(x.ravel(), 8), truth)
+    for extra in range(8):
+        x = np.hstack([inputs.FFA_IN_88, np.zeros((8, extra))])
+        truth = np.hstack([inputs.FFA_OUT_88, np.zeros((8, extra))])
+        assert np.array_equal(rt.ffa2(x), truth)
+
+
+@pytest.mark.parametrize("m,p,seed", inputs.FFA_CASES)
+def test_ffa2_golden_bit_exact(rt, golden, m, p, seed):
+    y = rt.ffa2(inputs.ffa_block(m, p, seed))
+    assert y.shape == (m, p) and y.dtype == np.float32
+    assert sha(y) == str(golden[f"ffa2_{m}x{p}_sha"])
+
+
+@pytest.mark.parametrize("m,p", [(1, 1), (2, 1), (7, 3), (33, 64), (150, 260), (1023, 34), (1025, 34),
+                                 (5000, 260), (21474, 240), (134217, 16), (3000, 17), (777, 4000),
+                                 (40, 12000), (9, 70000)])
+def test_ffa2_vs_oracle(rt, oracle, m, p):
+    x = np.random.RandomState(m * 31 + p).normal(size=(m, p)).astype(np.float32)
+    assert np.array_equal(rt.ffa2(x), oracle.ffa2(x))
+
+
+def test_ffa2_edge_and_errors(rt):
+    assert rt.ffa2(np.zeros((0, 5), np.float32)).shape == (0, 5)
+    with pytest.raises(ValueError):
+        rt.ffa2(np.zeros(4))
+    with pytest.raises(ValueError):
+        rt.ffa1(np.zeros((4, 4)), 4)
+    with pytest.raises(ValueError):
+        rt.ffa1(np.zeros(10), 11)
+    with pytest.raises(ValueError):
+        rt.ffa1(np.zeros(10), 4.0)
+    with pytest.raises(ValueError):
+        rt.ffa2(np.zeros((16, 8), np.float32)[:, ::2])   # non-contiguous float32
+
+
+# ---------------------------------------------------------------- downsample
+@pytest.mark.parametrize("f", inputs.DS_FACTORS)
+def test_downsample(rt, oracle, golden, f):
+    x = inputs.noise(20000, 11)
+    out = rt.downsample(x, f)
+    assert np.array_equal(out, oracle.downsample(x, f))          # strict restatement: bit-exact
+    assert np.allclose(out, golden[f"downsample_{f!r}"], rtol=2e-6, atol=2e-5 * max(1.0, f ** 0.5))
+
+
+def test_downsample_errors(rt):
+    x = np.zeros(100, np.float32)
+    for f in (0.55, 1.0, 101.0):
+        with pytest.raises(ValueError):
+            rt.downsample(x, f)
+
+
+# ---------------------------------------------------------------- S/N
+def test_snr2_golden(rt, oracle, golden):
+    prof = inputs.noise(200 * 250, 12).reshape(200, 250)
+    prof[:, 100:113] += 3.0
+    out = rt.boxcar_snr(prof, inputs.SNR_WIDTHS, 1.7)
+    ok, msg = snr_close(out, golden["snr2_out"])
+    assert ok, msg
+    ok, msg = snr_close(out, oracle.snr2(prof, inputs.SNR_WIDTHS, 1.7), rtol=2e-6)
+    assert ok, msg
+
+
+def test_snr_reference_cases(rt):
+    # test_snr.py:7-78
+    data = np.zeros(32, np.float32)
+    for bad in ([0, 1], [1, 32]):
+        with pytest.raises(ValueError):
+            rt.boxcar_snr(data, bad)
+    with pytest.raises(ValueError):
+        rt.boxcar_snr(data, [1, 2], stdnoise=-42.0)
+    assert rt.boxcar_snr(np.zeros((3, 4, 32), np.float32), [1, 2, 3, 5]).shape == (3, 4, 4)
+    rows = np.random.RandomState(0).normal(size=(4, 32)).astype(np.float32)
+    ref = rt.boxcar_snr(rows, [1, 2, 5, 11, 18, 31])
+    for shift in range(1, 33):
+        assert np.allclose(rt.boxcar_snr(np.roll(rows, shift, axis=-1), [1, 2, 5, 11, 18, 31]), ref)
+    n = 64
+    widths = np.arange(1, n)
+    d = np.zeros(n, np.float32)
+    for w in range(1, n):
+        d[:w] = 1.0
+        s = rt.boxcar_snr(d, widths)
+        assert s.argmax() == w - 1
+        assert np.allclose(s.max(), w * np.sqrt((n - w) / (n * w)))
+
+
+def test_circular_prefix_sum_and_rollback(rt, golden):
+    from riptide_amd import libcpp
+    prof = inputs.noise(200 * 250, 12).reshape(200, 250)
+    prof[:, 100:113] += 3.0
+    assert np.allclose(libcpp.circular_prefix_sum(prof[0].copy(), 700), golden["cps_out"], rtol=1e-6, atol=1e-5)
+    x = np.arange(10, dtype=np.float32)
+    y = np.arange(10, dtype=np.float32) * 10
+    for s in (0, 3, 10, 13):
+        assert np.array_equal(libcpp.rollback(x, s), np.roll(x, -s))
+        assert np.array_equal(libcpp.fused_rollback_add(x, y, s), x + np.roll(y, -s))
+    with pytest.raises(ValueError):
+        libcpp.fused_rollback_add(x, y[:5], 1)
+
+
+# ---------------------------------------------------------------- running median
+@pytest.mark.parametrize("w", inputs.RMED_WIDTHS)
+def test_running_median_exact(rt, golden, w):
+    assert np.array_equal(rt.running_median(inputs.noise(1000, 13), w), golden[f"rmed_{w}"])
+
+
+def test_running_median_reference_cases(rt):
+    # test_running_median.py:16-73
+    data = np.arange(10, dtype=np.float32)
+    for args in ((data, 2), (data, 10), (np.zeros((4, 8)), 3)):
+        with pytest.raises(ValueError):
+            rt.running_median(*args)
+    rs = np.random.RandomState(5)
+    x = rs.normal(size=300).reshape(100, 3).astype(np.float32)
+    for col in x.T:                 # non-contiguous slices
+        for w in (1, 3, 5, 7, 11, 25, 37):
+            padded = np.pad(col, (w // 2, w // 2), mode="edge")
+            naive = np.array([np.median(padded[i:i + w]) for i in range(col.size)])
+            assert np.array_equal(rt.running_median(col, w), naive)
+    with pytest.raises(ValueError):
+        rt.fast_running_median(np.zeros(100), 3, min_points=10)
+    x64 = rs.normal(size=100)
+    for w in (1, 3, 5, 7, 11, 25, 37):
+        assert np.array_equal(rt.running_median(x64, w), rt.fast_running_median(x64, w, min_points=39))
+
+
+@pytest.mark.parametrize("ws,mp", inputs.FAST_RMED_CASES)
+def test_fast_running_median_exact(rt, golden, ws, mp):
+    out = rt.fast_running_median(inputs.noise(30011, 14), ws, mp)
+    assert np.array_equal(out, golden[f"frmed_{ws}_{mp}"])
+
+
+# ---------------------------------------------------------------- periodogram
+@pytest.mark.parametrize("case", inputs.PGRAM_CASES, ids=lambda c: c["name"])
+def test_periodogram_golden(rt, oracle, golden, case):
+    from riptide_amd import libcpp
+    name = case["name"]
+    data = inputs.pgram_input(case)
+    widths = golden[f"pg_{name}_widths"]
+    periods, foldbins, snrs = libcpp.periodogram(data, case["tsamp"], widths, case["pmin"], case["pmax"],
+                                                 case["bmin"], case["bmax"])
+    assert np.array_equal(periods, golden[f"pg_{name}_periods"])
+    assert np.array_equal(foldbins, golden[f"pg_{name}_foldbins"])
+    ok, msg = snr_close(snrs, golden[f"pg_{name}_snrs"])
+    assert ok, msg
+    _, _, osnrs = oracle.periodogram(data, case["tsamp"], widths, case["pmin"], case["pmax"],
+                                     case["bmin"], case["bmax"])
+    ok, msg = snr_close(snrs, osnrs, rtol=2e-6)
+    assert ok, msg
+
+
+@pytest.mark.parametrize("case", inputs.SEARCH_CASES, ids=lambda c: c["name"])
+def test_ffa_search_pipeline(rt, golden, case):
+    name = case["name"]
+    raw = inputs.search_input(case)
+    ts = rt.TimeSeries(raw, case["tsamp"])
+    tsdr, pg = rt.ffa_search(ts, period_min=case["pmin"], period_max=case["pmax"], bins_min=case["bmin"],
+                             bins_max=case["bmax"], ducy_max=case["ducy_max"], rmed_width=case["rmed_width"],
+                             rmed_minpts=case["rmed_minpts"])
+    head = golden[f"search_{name}_normalised_head"]
+    assert np.allclose(tsdr.data[:head.size], head, rtol=0, atol=2e-6)
+    assert sha(pg.periods) == str(golden[f"search_{name}_periods_sha"])
+    ok, msg = snr_close(pg.snrs, golden[f"search_{name}_snrs"])
+    assert ok, msg
+    pg.metadata["dm"] = 0.0
+    peaks, _ = rt.find_peaks(pg)
+    ref = golden[f"search_{name}_peaks"]
+    got = np.array([(p.ip, p.iw, p.snr) for p in peaks], dtype=np.float64).reshape(-1, 3)
+    assert got.shape == ref.shape
+    assert np.array_equal(got[:, :2], ref[:, :2])           # identical candidate list
+    assert np.allclose(got[:, 2], ref[:, 2], rtol=1e-4, atol=1e-4)
+
+
+def test_ffa_search_reference_invariants(rt):
+    # test_ffa_search_pgram.py:11-96
+    np.random.seed(0)
+    ts = rt.TimeSeries.generate(200.0, 0.001, 1.0, amplitude=20.0)
+    tsdr, pg = rt.ffa_search(ts, period_min=0.8, period_max=1.2, bins_min=240, bins_max=260)
+    assert np.all(np.maximum.accumulate(pg.periods) == pg.periods)
+    assert pg.snrs.shape == (len(pg.periods), len(pg.widths))
+    assert pg.metadata == ts.metadata == tsdr.metadata
+    assert pg.tobs == 200.0
+    assert np.all(pg.freqs == 1.0 / pg.periods)
+    tsdr, pg = rt.ffa_search(ts, period_min=0.8, period_max=1.2, bins_min=240, bins_max=260,
+                             already_normalised=True, deredden=False)
+    assert id(tsdr) == id(ts)
+    # no downsampling: period_min = bins_min * tsamp (f == 1 rung)
+    rt.ffa_search(ts, period_min=0.8, period_max=1.2, bins_min=800, bins_max=1200)
+
+
+def test_periodogram_errors(rt):
+    from riptide_amd import libcpp
+    x = np.zeros(10000, np.float32)
+    w = np.array([1, 2], dtype=np.uint64)
+    bad = [(0.0, 1.0, 2.0), (1e-3, 0.0, 2.0), (1e-3, 1.0, 0.5), (1e-3, 0.01, 2.0)]
+    for tsamp, pmin, pmax in bad:
+        with pytest.raises(ValueError):
+            libcpp.periodogram(x, tsamp, w, pmin, pmax, 240, 260)
+    with pytest.raises(ValueError):
+        libcpp.periodogram(x, 1e-3, w, 1.0, 2.0, 1, 260)
+    with pytest.raises(ValueError):
+        libcpp.periodogram(x, 1e-3, w, 1.0, 2.0, 240, 200)
+
+
+# ---------------------------------------------------------------- device batch API
+def test_batch_matches_single(rt):
+    import torch
+    from riptide_amd import engine
+    case = inputs.PGRAM_CASES[1]
+    plan = engine.PeriodogramPlan.for_search(case["n"], case["tsamp"], case["pmin"], case["pmax"],
+                                             case["bmin"], case["bmax"], ducy_max=case["ducy_max"])
+    xs = np.stack([inputs.with_signal(case["n"], case["tsamp"], s, 0.41, 12.0) for s in range(5)])
+    d = torch.from_numpy(xs).cuda()
+    batch = plan.run(d).cpu().numpy()
+    from riptide_amd import libcpp
+    for b in range(5):
+        _, _, single = libcpp.periodogram(xs[b], case["tsamp"], plan.widths, case["pmin"], case["pmax"],
+                                          case["bmin"], case["bmax"])
+        assert np.array_equal(batch[b], single)
+    dn = engine.deredden_normalise(d, 1001, 101)
+    for b in range(2):
+        ref = libcpp.deredden_normalise(xs[b], 1001, 101)
+        assert np.array_equal(dn[b].cpu().numpy(), ref)
+
+
+# ---------------------------------------------------------------- full-size BASELINE configs
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3", "cfg4"])
+def test_full_config(rt, golden_full, name):
+    import torch
+    from riptide_amd import engine
+    g = golden_full["configs"][name]
+    c = g["case"]
+    raw = inputs.full_input(c)
+    if sha(raw) != g["input_sha"]:
+        pytest.skip("input generator differs on this host (numpy RNG/libm); parity not checkable")
+    plan = engine.PeriodogramPlan.for_search(c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"],
+                                             ducy_max=c["ducy_max"])
+    assert [int(w) for w in plan.widths] == g["widths"] and plan.length == g["length"]
+    periods, foldbins = plan.grid()
+    assert sha(periods) == g["periods_sha"] and sha(foldbins) == g["foldbins_sha"]
+    d = torch.from_numpy(raw).cuda()
+    x = engine.deredden_normalise(d, int(round(4.0 / c["tsamp"])), 101)
+    snrs = plan.run(x).cpu().numpy()
+    rows = np.asarray(g["sample_rows"])
+    ok, msg = snr_close(snrs[rows], np.asarray(g["sample_snrs"], dtype=np.float32))
+    assert ok, msg
+    assert np.allclose(snrs.max(axis=0), g["snr_max"], rtol=1e-4)
+    assert list(snrs.argmax(axis=0)) == g["snr_argmax"]
+    pg = rt.Periodogram(plan.widths, periods, foldbins, snrs, metadata=rt.Metadata({"tobs": c["n"] * c["tsamp"],
+                                                                                       "dm": 0.0}))
+    peaks, _ = rt.find_peaks(pg)
+    got = [[p.ip, p.iw] for p in peaks]
+    assert got == [[p[0], p[1]] for p in g["peaks"]]     # identical candidate list

@@ -1,0 +1,192 @@
+"""CPU-only tests: the C-ABI library loads and exports every symbol of
+include/riptide_amd.h; the host planner (ladder, trial grid, pass schedule) is
+bit-exact with the reference; host-side Python logic (width trials, ffafreq,
+clustering, peak detection, argument validation) matches the reference.
+No compute call reaches the GPU here."""
+import ctypes
+import hashlib
+import os
+import re
+
+import numpy as np
+import pytest
+
+import inputs
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "riptide_amd.h")
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from riptide_amd import _lib
+    return _lib.load()
+
+
+def test_header_symbols_exported(lib):
+    text = open(HEADER).read()
+    declared = set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\**(rt_\w+)\s*\(", text, re.M))
+    assert len(declared) >= 25
+    from riptide_amd import _lib
+    for name in declared:
+        assert hasattr(lib, name), name
+        assert name in _lib.EXPORTED, f"{name} has no ctypes signature"
+    # and nothing in the loader that the header does not declare
+    assert set(_lib.EXPORTED) <= declared
+
+
+def test_version(lib):
+    assert b"gfx950" in lib.rt_version()
+
+
+def _grid(lib, c):
+    L = ctypes.c_size_t()
+    rc = lib.rt_periodogram_length(c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"], ctypes.byref(L))
+    assert rc == 0
+    periods = np.empty(L.value, np.float64)
+    foldbins = np.empty(L.value, np.uint32)
+    from riptide_amd._lib import ptr
+    assert lib.rt_periodogram_grid(c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"],
+                                   ptr(periods), ptr(foldbins)) == 0
+    return periods, foldbins
+
+
+@pytest.mark.parametrize("case", inputs.PGRAM_CASES, ids=lambda c: c["name"])
+def test_grid_small_bit_exact(lib, golden, case):
+    periods, foldbins = _grid(lib, case)
+    assert np.array_equal(periods, golden[f"pg_{case['name']}_periods"])
+    assert np.array_equal(foldbins, golden[f"pg_{case['name']}_foldbins"])
+
+
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3", "cfg4"])
+def test_grid_full_bit_exact(lib, golden_full, name):
+    g = golden_full["configs"][name]
+    periods, foldbins = _grid(lib, g["case"])
+    assert periods.size == g["length"]
+    assert sha(periods) == g["periods_sha"]
+    assert sha(foldbins) == g["foldbins_sha"]
+
+
+@pytest.mark.parametrize("case", inputs.FULL_CASES + inputs.PGRAM_CASES + inputs.SEARCH_CASES,
+                         ids=lambda c: c["name"] + str(c["n"]))
+def test_schedule_invariants(lib, case):
+    u = [ctypes.c_uint64() for _ in range(4)]
+    d = [ctypes.c_double() for _ in range(2)]
+    rc = lib.rt_schedule_check(case["n"], case["tsamp"], 10, case["pmin"], case["pmax"], case["bmin"], case["bmax"],
+                               ctypes.byref(u[0]), ctypes.byref(u[1]), ctypes.byref(u[2]), ctypes.byref(d[0]),
+                               ctypes.byref(d[1]), ctypes.byref(u[3]))
+    assert rc == 0, lib.rt_last_error()
+    assert u[1].value >= u[0].value > 0
+    # actual traffic stays within 1.6x the SURVEY.md §8(d) algorithmic bytes
+    assert d[1].value <= 1.6 * d[0].value
+
+
+def test_schedule_cfg2_shape(lib):
+    """cfg2 (headline): every cell of every transform is transformed; the plan
+    has the documented size (1153 transforms, 1331.6 M cells)."""
+    u = [ctypes.c_uint64() for _ in range(4)]
+    d = [ctypes.c_double() for _ in range(2)]
+    assert lib.rt_schedule_check(1 << 23, 256e-6, 6, 0.1, 10.0, 240, 260, *(ctypes.byref(x) for x in u[:3]),
+                                 ctypes.byref(d[0]), ctypes.byref(d[1]), ctypes.byref(u[3])) == 0
+    assert u[0].value == 1153
+    assert abs(u[3].value / 1e6 - 1331.6) < 0.1
+
+
+def test_periodogram_length_errors(lib):
+    from riptide_amd import _lib
+    L = ctypes.c_size_t()
+    cases = [(0.0, 1.0, 2.0, 240, 260, "tsamp must be > 0"),
+             (1e-3, 0.0, 2.0, 240, 260, "period_min must be > 0"),
+             (1e-3, 1.0, 0.5, 240, 260, "period_max must be > period_min"),
+             (1e-3, 1.0, 2.0, 1, 260, "bins_min must be > 1"),
+             (1e-3, 1.0, 2.0, 240, 200, "bins_max must be >= bins_min"),
+             (1e-3, 0.1, 2.0, 240, 260, "Must have: period_min >= tsamp * bins_min")]
+    for tsamp, pmin, pmax, bmin, bmax, msg in cases:
+        rc = lib.rt_periodogram_length(10000, tsamp, pmin, pmax, bmin, bmax, ctypes.byref(L))
+        assert rc == _lib.RT_EINVAL
+        assert lib.rt_last_error().decode().startswith(msg)
+
+
+def test_width_trials():
+    from riptide_amd import generate_width_trials
+    assert list(generate_width_trials(240, ducy_max=0.05)) == [1, 2, 3, 4, 6, 9]
+    assert list(generate_width_trials(240)) == [1, 2, 3, 4, 6, 9, 13, 19, 28, 42]
+    assert list(generate_width_trials(16)) == [1, 2, 3]
+
+
+def test_ffafreq():
+    # test_ffa_base_functions.py:78-118
+    from riptide_amd import ffafreq, ffaprd
+    m, p = 42, 127
+    dt = np.pi / 1000.0
+    s = np.arange(m, dtype=float)
+    true_periods = p ** 2 / (p - s / (m - 1.0)) * dt
+    assert np.allclose(ffafreq(m * p, p, dt=dt), 1.0 / true_periods)
+    assert np.allclose(ffaprd(m * p, p, dt=dt), true_periods)
+    assert ffafreq(p, p, dt=dt)[0] == 1.0 / (p * dt)
+    for args in ((0, p), (np.pi, p), (m * p, 1), (m * p, np.pi), (m * p, m * p + 1)):
+        with pytest.raises(ValueError):
+            ffafreq(*args, dt=dt)
+    with pytest.raises(ValueError):
+        ffafreq(m * p, p, dt=0)
+
+
+def test_cluster1d():
+    from riptide_amd import cluster1d
+    assert cluster1d(np.array([]), 1.0) == []
+    x = np.array([5.0, 1.0, 1.5, 9.0, 5.2])
+    cl = cluster1d(x, 0.6)
+    assert [sorted(c.tolist()) for c in cl] == [[1, 2], [0, 4], [3]]
+    assert [c.tolist() for c in cluster1d(np.array([1.0, 1.1, 1.2]), 0.5)] == [[0, 1, 2]]
+
+
+def test_find_peaks_on_reference_snr(golden):
+    """Host peak detection on the REFERENCE's S/N reproduces the reference's
+    candidate list exactly (the logic is unchanged; see peak_detection.py)."""
+    from riptide_amd import Metadata, Periodogram, find_peaks
+    for case in inputs.SEARCH_CASES:
+        name = case["name"]
+        from riptide_amd._lib import load, ptr
+        lib = load()
+        L = ctypes.c_size_t()
+        lib.rt_periodogram_length(case["n"], case["tsamp"], case["pmin"], case["pmax"], case["bmin"],
+                                  case["bmax"], ctypes.byref(L))
+        periods = np.empty(L.value)
+        foldbins = np.empty(L.value, np.uint32)
+        lib.rt_periodogram_grid(case["n"], case["tsamp"], case["pmin"], case["pmax"], case["bmin"], case["bmax"],
+                                ptr(periods), ptr(foldbins))
+        snrs = golden[f"search_{name}_snrs"]
+        from riptide_amd import generate_width_trials
+        widths = generate_width_trials(case["bmin"], ducy_max=case["ducy_max"])
+        pg = Periodogram(widths, periods, foldbins, snrs, metadata=Metadata({"tobs": case["n"] * case["tsamp"],
+                                                                             "dm": 0.0}))
+        peaks, _ = find_peaks(pg)
+        got = np.array([(p.ip, p.iw, p.snr) for p in peaks], dtype=np.float64).reshape(-1, 3)
+        assert np.array_equal(got, golden[f"search_{name}_peaks"])
+
+
+def test_shim_validation_before_device():
+    """Argument errors of the drop-in are raised before any device work."""
+    from riptide_amd import libcpp
+    with pytest.raises(ValueError, match="contiguous"):
+        libcpp.ffa2(np.zeros((8, 8), np.float32)[:, ::2])
+    with pytest.raises(ValueError, match="incorrect number of dimensions"):
+        libcpp.ffa2(np.zeros(8, np.float32))
+    with pytest.raises(ValueError, match="same number of elements"):
+        libcpp.fused_rollback_add(np.zeros(3), np.zeros(4), 1)
+    with pytest.raises(ValueError, match="Downsampling factor"):
+        libcpp.downsample(np.zeros(10, np.float32), 0.5)
+
+
+def test_periodogram_object():
+    from riptide_amd import Metadata, Periodogram
+    pg = Periodogram(np.array([1, 2]), np.array([1.0, 2.0]), np.array([240, 240], np.uint32),
+                     np.zeros((2, 2), np.float32), metadata=Metadata({"tobs": 10.0}))
+    assert np.array_equal(pg.freqs, [1.0, 0.5])
+    assert pg.tobs == 10.0
+    assert Periodogram.from_dict(pg.to_dict()).metadata == pg.metadata
+    assert Metadata({})["dm"] is None
