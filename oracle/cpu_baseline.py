@@ -20,6 +20,8 @@ import time
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+# run as a script: drop oracle/ itself from the path so `oracle` is the package
+sys.path = [p for p in sys.path if os.path.abspath(p or '.') != HERE]
 sys.path.insert(0, os.path.dirname(HERE))
 
 

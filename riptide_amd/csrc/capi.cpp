@@ -311,7 +311,8 @@ rt_plan* make_plan(size_t size, double tsamp, const uint64_t* widths, size_t nw,
             d.out_off = R.leaf_off;
             d.first_block = blocks;
             d.identity = R.f == 1.0;
-            blocks += (uint32_t)((R.n + 255) / 256);
+            ds_configure(d);
+            blocks += (uint32_t)((R.n + d.per_block - 1) / d.per_block);
             P->rungs.push_back(d);
         }
         P->ds_blocks = blocks;
@@ -612,9 +613,11 @@ int rt_downsample(const float* x, size_t size, double f, float* out)
         r.f = f;
         r.n = n;
         r.first_block = 0;
+        ds_configure(r);
         h2d(dx, x, size * 4, c.stream);
         h2d(dr, &r, sizeof r, c.stream);
-        ck(launch_downsample_ladder(dx, size, size, dr, 1, (uint32_t)((n + 255) / 256), dz, n, 1, c.stream),
+        ck(launch_downsample_ladder(dx, size, size, dr, 1, (uint32_t)((n + r.per_block - 1) / r.per_block), dz, n,
+                                    1, c.stream),
            "downsample");
         d2h(out, dz, n * 4, c.stream);
         sync(c.stream);

@@ -30,6 +30,7 @@ constexpr int kMaxRanges = (1 << (kMaxTileLevels + 1)) - 1;
 constexpr int kMaxWholeLevels = 11;         // ceil(log2(kMaxRows)) + 1
 constexpr int kMaxWidths = 32;           // boxcar widths handled by the fused S/N epilogue
 constexpr int kRegsPerThread = (kLdsDataFloats + kConeBlock - 1) / kConeBlock;
+constexpr int kMergeGroup = 8;             // elements per thread with LDS reads in flight together
 
 // Row capacity of the LDS level buffer for p phase bins.
 inline int lds_row_capacity(uint32_t p)

@@ -16,13 +16,17 @@ namespace rt {
 // ---------------------------------------------------------------------------
 // Downsampling ladder (downsample.hpp:44-82; periodogram.hpp:162-168)
 // ---------------------------------------------------------------------------
-// One thread per output sample of one rung of one trial.  Rungs are flattened
-// along blockIdx.x through a per-rung first-block table; blockIdx.y = trial.
+// One block = up to 256 consecutive outputs of one rung of one trial (fewer for
+// large f, so the block's input span fits the LDS stage).  The span is loaded
+// with coalesced loads, then each thread sums its window from LDS in the
+// reference's order.  Rungs are flattened along blockIdx.x through a per-rung
+// first-block table; blockIdx.y = trial.
 __global__ __launch_bounds__(256) void downsample_ladder_kernel(
     const float* __restrict__ x, uint64_t n_in, uint64_t x_stride,
     const DsRung* __restrict__ rungs, uint32_t num_rungs,
     float* __restrict__ out, uint64_t out_stride)
 {
+    __shared__ float span[kDsSpanFloats];
     uint32_t lo = 0, hi = num_rungs - 1;
     const uint32_t b = blockIdx.x;
     while (lo < hi) {
@@ -30,28 +34,44 @@ __global__ __launch_bounds__(256) void downsample_ladder_kernel(
         if (rungs[mid].first_block <= b) lo = mid; else hi = mid - 1;
     }
     const DsRung r = rungs[lo];
-    const uint64_t k = (uint64_t)(b - r.first_block) * 256 + threadIdx.x;
-    if (k >= r.n) return;
+    const uint64_t k0 = (uint64_t)(b - r.first_block) * r.per_block;
+    const uint64_t k1 = min(k0 + r.per_block, r.n);
     x += (uint64_t)blockIdx.y * x_stride;
     out += (uint64_t)blockIdx.y * out_stride + r.out_off;
+    const uint64_t k = k0 + threadIdx.x;
     if (r.identity) {           // f == 1: the rung searches the data at its own resolution
-        out[k] = x[k];
+        if (k < k1) out[k] = x[k];
         return;
     }
     const double f = r.f;
+    const double last = (double)n_in - 1.0;
+    // input span of the block: [imin(k0), imax(k1 - 1)]
+    const uint64_t s0 = (uint64_t)floor(__dmul_rn((double)k0, f));
+    double e1 = floor(__dadd_rn(__dmul_rn((double)(k1 - 1), f), f));
+    if (e1 > last) e1 = last;
+    const uint64_t s1 = (uint64_t)e1;
+    const float* src = x + s0;
+    if (r.staged) {
+        const uint32_t len = (uint32_t)(s1 - s0 + 1);
+        for (uint32_t i = threadIdx.x; i < len; i += 256) span[i] = x[s0 + i];
+        __syncthreads();
+        src = span;
+    }
+    if (k >= k1) return;
     const double start = __dmul_rn((double)k, f);
     const double end = __dadd_rn(start, f);
     const uint64_t imin = (uint64_t)floor(start);
     double dmax = floor(end);
-    const double last = (double)n_in - 1.0;
     if (dmax > last) dmax = last;
     const uint64_t imax = (uint64_t)dmax;
     const float wmin = (float)__dsub_rn((double)(imin + 1), start);
     const float wmax = (float)__dsub_rn(end, (double)imax);
-    float acc = __fmul_rn(wmin, x[imin]);
-    for (uint64_t i = imin + 1; i < imax; ++i)
-        acc = __fadd_rn(acc, x[i]);
-    acc = __fadd_rn(acc, __fmul_rn(wmax, x[imax]));
+    const float* w = src + (imin - s0);
+    const uint32_t cnt = (uint32_t)(imax - imin);
+    float acc = __fmul_rn(wmin, w[0]);
+    for (uint32_t i = 1; i < cnt; ++i)
+        acc = __fadd_rn(acc, w[i]);
+    acc = __fadd_rn(acc, __fmul_rn(wmax, w[cnt]));
     out[k] = acc;
 }
 
@@ -154,6 +174,8 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
     const int L = it.levels;
     const bool tile = it.mode == kModeTile;
     const uint64_t trial = blockIdx.y;
+    // LDS row of -0.0f after the largest level the planner allows (lds_row_capacity)
+    const int zrow = (kLdsDataFloats / p - 1) * p;
 
     const float* src;
     if (it.src == kSelLeaves) src = a.leaves + trial * a.leaves_stride + X.src_off;
@@ -238,7 +260,7 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
         }
         __syncthreads();
         nrows = lv_rows[L];
-        if (nrows > kMaxRows || nrows * p > kLdsDataFloats) {
+        if (nrows > kMaxRows || nrows * p > zrow) {
             if (tid == 0 && a.error_flag) atomicOr(a.error_flag, 1);
             return;
         }
@@ -249,26 +271,48 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
             desc[r].x = R.start + R.lo + (r - R.base);
         }
         __syncthreads();
-        const int total = nrows * p;
-        for (int e = tid; e < total; e += kConeBlock) {
-            const int r = div_rows(e, p, inv_p);
-            const int col = e - r * p;
-            data[e] = src[(uint64_t)desc[r].x * p + col];
-        }
     } else {
         nrows = (int)it.node_size;
-        if (nrows > kMaxRows || nrows * p > kLdsDataFloats) {
+        if (nrows > kMaxRows || nrows * p > zrow) {
             if (tid == 0 && a.error_flag) atomicOr(a.error_flag, 2);
             return;
         }
-        const float* s = src + (uint64_t)it.node_start * p;
+    }
+    // ---- fill the bottom level: every thread issues all its global loads
+    // before the first LDS write (one HBM round trip per item, not per element)
+    {
         const int total = nrows * p;
-        for (int e = tid; e < total; e += kConeBlock) data[e] = s[e];
+        const float* base = tile ? src : src + (uint64_t)it.node_start * p;
+        float v[kRegsPerThread];
+        int r = div_rows(tid, p, inv_p);
+        int col = tid - r * p;
+        int rem = total - tid;
+        asm volatile("" : "+v"(r), "+v"(col), "+v"(rem));
+        const int dr = kConeBlock / p, dc = kConeBlock - (kConeBlock / p) * p;
+#pragma unroll
+        for (int k = 0; k < kRegsPerThread; ++k) {
+            if (rem > k * kConeBlock) {
+                const uint64_t off = tile ? (uint64_t)desc[r].x * p + col : (uint64_t)(k * kConeBlock + tid);
+                v[k] = base[off];
+            }
+            r += dr;
+            col += dc;
+            if (col >= p) {
+                col -= p;
+                ++r;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kRegsPerThread; ++k)
+            if (rem > k * kConeBlock) data[k * kConeBlock + tid] = v[k];
     }
     __syncthreads();
 
     // ---- merge levels, deepest first
     for (int l = L - 1; l >= 0; --l) {
+        if (l == L - 1) {
+            for (int i = tid; i < p; i += kConeBlock) data[zrow + i] = -0.0f;
+        }
         const int orows = tile ? lv_rows[l] : (int)it.node_size;
         for (int r = tid; r < orows; r += kConeBlock) {
             int hrow, trow = -1, shift = 0;
@@ -309,7 +353,7 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
                 }
             }
             const int ho = hrow * p;
-            const int to = trow < 0 ? 0xFFFF : trow * p;
+            const int to = trow < 0 ? zrow : trow * p;
             desc[r] = make_int2(ho | (to << 16), shift);
         }
         __syncthreads();
@@ -318,39 +362,45 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
         // (row, col) of element e = k * kConeBlock + tid, advanced incrementally
         int r = div_rows(tid, p, inv_p);
         int col = tid - r * p;
-        int rem = total - tid;
         // opaque per level: stops LICM from hoisting all per-element indices
         // out of the level loop (which spills the register file)
-        asm volatile("" : "+v"(r), "+v"(col), "+v"(rem));
+        asm volatile("" : "+v"(r), "+v"(col));
         const int dr = kConeBlock / p, dc = kConeBlock - (kConeBlock / p) * p;
+        const int last_row = orows - 1;
+        // Branch-free body, groups of kMergeGroup elements per thread: every
+        // group issues all its descriptor reads, then all its data reads, so the
+        // LDS latency is paid once per group.  Elements past the end of the
+        // level read a clamped (valid) row and are not written back.
 #pragma unroll
-        for (int k = 0; k < kRegsPerThread; ++k) {
-            if (rem > k * kConeBlock) {
-                const int2 d = desc[r];
-                const int ho = d.x & 0xFFFF;
-                const int to = (int)((unsigned)d.x >> 16);
-                float x = data[ho + col];
-                if (to != 0xFFFF) {
+        for (int g = 0; g < kRegsPerThread; g += kMergeGroup) {
+            if (g * kConeBlock < total) {          // uniform: whole group inactive otherwise
+#pragma unroll
+                for (int j = 0; j < kMergeGroup && g + j < kRegsPerThread; ++j) {
+                    const int2 d = desc[min(r, last_row)];
+                    const int ho = d.x & 0xFFFF;
+                    const int to = (int)((unsigned)d.x >> 16);
                     int c2 = col + d.y;
-                    if (c2 >= p) c2 -= p;
-                    x = __fadd_rn(x, data[to + c2]);
+                    c2 = c2 >= p ? c2 - p : c2;
+                    // carried rows point `to` at the -0.0 row: x + (-0.0) == x exactly
+                    v[g + j] = __fadd_rn(data[ho + col], data[to + c2]);
+                    r += dr;
+                    col += dc;
+                    const bool wrap = col >= p;
+                    col = wrap ? col - p : col;
+                    r = wrap ? r + 1 : r;
                 }
-                v[k] = x;
             }
-            r += dr;
-            col += dc;
-            if (col >= p) {
-                col -= p;
-                ++r;
-            }
-            // bound the live ranges: at most 4 elements' loads in flight per thread
-            if ((k & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < kRegsPerThread; ++k) {
-            const int e = k * kConeBlock + tid;
-            if (e < total) data[e] = v[k];
+        for (int g = 0; g < kRegsPerThread; g += kMergeGroup) {
+            if (g * kConeBlock < total) {
+#pragma unroll
+                for (int j = 0; j < kMergeGroup && g + j < kRegsPerThread; ++j) {
+                    const int e = (g + j) * kConeBlock + tid;
+                    if (e < total) data[e] = v[g + j];
+                }
+            }
         }
         __syncthreads();
         nrows = orows;
@@ -360,8 +410,14 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
     if (it.dst != kSelSnr) {
         float* dst = (it.dst == kSelPing ? a.ping : a.pong) + trial * a.buf_stride + X.buf_off +
                      (uint64_t)(it.node_start + it.s0) * p;
-        const int total = nrows * p;
-        for (int e = tid; e < total; e += kConeBlock) dst[e] = data[e];
+        const int rem = nrows * p - tid;
+        float v[kRegsPerThread];
+#pragma unroll
+        for (int k = 0; k < kRegsPerThread; ++k)
+            if (rem > k * kConeBlock) v[k] = data[k * kConeBlock + tid];
+#pragma unroll
+        for (int k = 0; k < kRegsPerThread; ++k)
+            if (rem > k * kConeBlock) dst[k * kConeBlock + tid] = v[k];
         return;
     }
 

@@ -2,9 +2,13 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cmath>
+
 #include "common.hpp"
 
 namespace rt {
+
+constexpr uint32_t kDsSpanFloats = 8192;   // LDS input stage of the ladder kernel (32 KiB)
 
 struct DsRung {
     double f;
@@ -12,7 +16,24 @@ struct DsRung {
     uint64_t out_off;    // float offset in the per-trial leaf buffer
     uint32_t first_block;
     uint32_t identity;   // f == 1: plain copy
+    uint32_t per_block;  // outputs per block (input span of a block <= kDsSpanFloats)
+    uint32_t staged;     // 0: f too large to stage a block's span in LDS, read global memory
 };
+
+// Outputs per block of the ladder kernel for factor f (0: cannot stage).
+inline uint32_t ds_per_block(double f)
+{
+    const double o = std::floor((double)(kDsSpanFloats - 4) / (f + 1.0)) - 1.0;
+    if (o < 1.0) return 0;
+    return o > 256.0 ? 256u : (uint32_t)o;
+}
+
+inline void ds_configure(DsRung& r)
+{
+    const uint32_t o = r.identity ? 256u : ds_per_block(r.f);
+    r.staged = o != 0;
+    r.per_block = o ? o : 256u;
+}
 
 // ffa_kernels.hip
 hipError_t launch_downsample_ladder(const float* x, uint64_t n_in, uint64_t x_stride,

@@ -154,9 +154,9 @@ ConeNeed cone_need(uint32_t node_size, uint32_t s0, uint32_t s1, int levels, uin
     return need;
 }
 
-static bool fits(const ConeNeed& n)
+static bool fits(const ConeNeed& n, uint32_t p)
 {
-    return n.max_rows <= kMaxRows && n.max_floats <= kLdsDataFloats && n.ranges <= kMaxRanges;
+    return n.max_rows <= lds_row_capacity(p) && n.max_floats <= kLdsDataFloats && n.ranges <= kMaxRanges;
 }
 
 // Per-transform schedule: list of passes, each a list of (node, tile, levels).
@@ -216,14 +216,14 @@ static void plan_transform(const FfaXform& X, uint32_t xi, std::vector<PassItems
             while (s0 < n.size) {
                 uint32_t K = std::min<uint32_t>((uint32_t)guess, n.size - s0);
                 ConeNeed need = cone_need(n.size, s0, s0 + K, L, p);
-                while (K > 1 && !fits(need)) {
+                while (K > 1 && !fits(need, p)) {
                     K -= std::max<uint32_t>(1, K / 32);
                     need = cone_need(n.size, s0, s0 + K, L, p);
                 }
-                if (!fits(need)) throw std::invalid_argument("cone tile does not fit in LDS");
+                if (!fits(need, p)) throw std::invalid_argument("cone tile does not fit in LDS");
                 while (s0 + K < n.size) {
                     ConeNeed nn = cone_need(n.size, s0, s0 + K + 1, L, p);
-                    if (!fits(nn)) break;
+                    if (!fits(nn, p)) break;
                     need = nn;
                     ++K;
                 }
