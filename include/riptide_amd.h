@@ -154,6 +154,12 @@ int rt_profile_enable(int on);
 int rt_profile_read(int kind, double* milliseconds, double* alg_bytes, double* moved_bytes, uint64_t* launches);
 int rt_profile_reset(void);
 
+/* Diagnostics (meaningful in the -DRT_STAMPS build, libriptide_amd_stamps.so):
+ * cone-kernel cycles per phase summed over work items -- [0] prologue,
+ * [1] bottom-level fill, [2] row descriptors, [3] merge levels, [4] store,
+ * [5] fused S/N, [7] items.  The first call allocates the counters. */
+int rt_diag_stamps(uint64_t* out8, int reset);
+
 /* Plan statistics: transforms, work items, passes, cone launches per trial. */
 int rt_plan_stats(const rt_plan* plan, uint64_t* transforms, uint64_t* items, uint64_t* launches,
                   double* alg_bytes_per_trial, double* moved_bytes_per_trial, uint64_t* cells_per_trial);

@@ -9,7 +9,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libriptide_amd.so")
+LIB_PATH = os.environ.get("RIPTIDE_AMD_LIB") or os.path.join(_HERE, "libriptide_amd.so")
 
 RT_OK, RT_EINVAL, RT_EHIP, RT_EINTERNAL = 0, 1, 2, 3
 
@@ -57,6 +57,7 @@ _SIGNATURES = {
     "rt_profile_enable": (_c_i, [_c_i]),
     "rt_profile_read": (_c_i, [_c_i, _pd, _pd, _pd, _pu64]),
     "rt_profile_reset": (_c_i, []),
+    "rt_diag_stamps": (_c_i, [_pu64, _c_i]),
     "rt_plan_stats": (_c_i, [_vp, _pu64, _pu64, _pu64, _pd, _pd, _pu64]),
 }
 

@@ -161,10 +161,14 @@ struct DevicePlan {
     }
 };
 
+// Per-phase cycle counters of the cone kernel (RT_STAMPS diagnostic builds).
+unsigned long long* g_stamps = nullptr;
+
 // Run all cone launches of an exec plan.
 void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStream_t s)
 {
     a.xf = P.d_xf;
+    a.stamps = g_stamps;
     for (const Launch& L : P.ex.launches) {
         a.items = P.d_items + L.first;
         a.num_items = L.count;
@@ -925,6 +929,20 @@ int rt_profile_read(int kind, double* ms, double* alg, double* moved, uint64_t* 
         *alg = b;
         *moved = mv;
         *launches = g_prof.rec[kind].size();
+        return RT_OK;
+    });
+}
+
+int rt_diag_stamps(uint64_t* out8, int reset)
+{
+    return guarded([&] {
+        if (!g_stamps) {
+            ck(hipMalloc(&g_stamps, 8 * sizeof(unsigned long long)), "hipMalloc");
+            ck(hipMemset(g_stamps, 0, 8 * sizeof(unsigned long long)), "hipMemset");
+        }
+        ck(hipDeviceSynchronize(), "hipDeviceSynchronize");
+        ck(hipMemcpy(out8, g_stamps, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost), "hipMemcpy");
+        if (reset) ck(hipMemset(g_stamps, 0, 8 * sizeof(unsigned long long)), "hipMemset");
         return RT_OK;
     });
 }

@@ -19,6 +19,12 @@
 #include <cstddef>
 #include <cstdint>
 
+#if defined(__HIPCC__)
+#define RT_HD __host__ __device__
+#else
+#define RT_HD
+#endif
+
 namespace rt {
 
 // ---- cone kernel geometry (gfx950: 160 KiB LDS per CU, one workgroup per CU)
@@ -30,12 +36,20 @@ constexpr int kMaxRanges = (1 << (kMaxTileLevels + 1)) - 1;
 constexpr int kMaxWholeLevels = 11;         // ceil(log2(kMaxRows)) + 1
 constexpr int kMaxWidths = 32;           // boxcar widths handled by the fused S/N epilogue
 constexpr int kRegsPerThread = (kLdsDataFloats + kConeBlock - 1) / kConeBlock;
+constexpr int kSnrChunk = 33;             // S/N epilogue: columns per lane held in registers
 constexpr int kMergeGroup = 8;             // elements per thread with LDS reads in flight together
 
-// Row capacity of the LDS level buffer for p phase bins.
-inline int lds_row_capacity(uint32_t p)
+constexpr int kQuadsPerThread = (kLdsDataFloats / 4 + kConeBlock - 1) / kConeBlock;
+
+// LDS rows are padded to a multiple of 4 floats (16-byte aligned rows) so the
+// merge can move 4 phase bins per lane with ds_read_b128 / ds_write_b128.
+RT_HD inline int lds_row_stride(uint32_t p) { return (int)((p + 3) & ~3u); }
+
+// Row capacity of the LDS level buffer for p phase bins (one row is kept free
+// for the -0.0 row that carried leaves add).
+RT_HD inline int lds_row_capacity(uint32_t p)
 {
-    const int c = kLdsDataFloats / (int)p - 1;   // -1: room for per-range alignment padding
+    const int c = kLdsDataFloats / lds_row_stride(p) - 1;
     return c < kMaxRows ? c : kMaxRows;
 }
 
@@ -85,6 +99,7 @@ struct ConeArgs {
     uint64_t snr_stride;
     uint32_t widths[kMaxWidths];  // boxcar widths (bins)
     int* error_flag;      // set non-zero if a work item violates the LDS budget
+    unsigned long long* stamps;   // RT_STAMPS diagnostic builds only: per-phase cycles
 };
 
 // Merge index of the FFA recursion (transforms.hpp:17-22): the reference build

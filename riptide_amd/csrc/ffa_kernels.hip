@@ -116,16 +116,6 @@ __device__ __forceinline__ int div_rows(int e, int p, float inv_p)
     return r;
 }
 
-__device__ __forceinline__ double wave_incl_scan(double v, int lane)
-{
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const double y = __shfl_up(v, o, 64);
-        if (lane >= o) v += y;
-    }
-    return v;
-}
-
 __device__ __forceinline__ int wave_incl_scan_int(int v, int lane)
 {
 #pragma unroll
@@ -133,14 +123,6 @@ __device__ __forceinline__ int wave_incl_scan_int(int v, int lane)
         const int y = __shfl_up(v, o, 64);
         if (lane >= o) v += y;
     }
-    return v;
-}
-
-__device__ __forceinline__ float wave_max(float v)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-        v = fmaxf(v, __shfl_xor(v, o, 64));
     return v;
 }
 
@@ -155,14 +137,34 @@ __device__ __forceinline__ int find_range(const Range* ranges, int first, int co
     return lo;
 }
 
+// Diagnostic build only (make stamps, -DRT_STAMPS): thread 0 adds the cycles of
+// each phase of the item to a.stamps[phase] (s_memtime; phases end at barriers).
+#ifdef RT_STAMPS
+#define RT_STAMP(i)                                                              \
+    do {                                                                         \
+        if (tid == 0) {                                                          \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();          \
+            atomicAdd(&a.stamps[i], t_ - t_stamp);                               \
+            t_stamp = t_;                                                        \
+        }                                                                        \
+    } while (0)
+#else
+#define RT_STAMP(i) do { } while (0)
+#endif
+
 __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
 {
-    __shared__ float data[kLdsDataFloats];
+#ifdef RT_STAMPS
+    unsigned long long t_stamp = __builtin_amdgcn_s_memtime();
+#endif
+    __shared__ float4 data4[kLdsDataFloats / 4];   // 16-byte aligned level buffer
+    float* const data = reinterpret_cast<float*>(data4);
     __shared__ int2 desc[kMaxRows];
     __shared__ Range ranges[kMaxRanges];
     __shared__ int lv_first[kMaxTileLevels + 1];
     __shared__ int lv_count[kMaxTileLevels + 1];
     __shared__ int lv_rows[kMaxTileLevels + 1];
+    __shared__ int wl[kMaxWidths];           // boxcar widths, staged in LDS (DS ops wait by count)
 
     const ConeItem it = a.items[blockIdx.x];
     const FfaXform X = a.xf[it.xform];
@@ -174,8 +176,11 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
     const int L = it.levels;
     const bool tile = it.mode == kModeTile;
     const uint64_t trial = blockIdx.y;
+    if (tid < kMaxWidths) wl[tid] = (int)a.widths[tid];
+    const int p4 = lds_row_stride((uint32_t)p);          // LDS row stride (floats)
+    const int qpr = p4 >> 2;                               // quads per LDS row
     // LDS row of -0.0f after the largest level the planner allows (lds_row_capacity)
-    const int zrow = (kLdsDataFloats / p - 1) * p;
+    const int zrow = (kLdsDataFloats / p4 - 1) * p4;
 
     const float* src;
     if (it.src == kSelLeaves) src = a.leaves + trial * a.leaves_stride + X.src_off;
@@ -260,7 +265,7 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
         }
         __syncthreads();
         nrows = lv_rows[L];
-        if (nrows > kMaxRows || nrows * p > zrow) {
+        if (nrows > kMaxRows || nrows * p4 > zrow) {
             if (tid == 0 && a.error_flag) atomicOr(a.error_flag, 1);
             return;
         }
@@ -273,11 +278,12 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
         __syncthreads();
     } else {
         nrows = (int)it.node_size;
-        if (nrows > kMaxRows || nrows * p > zrow) {
+        if (nrows > kMaxRows || nrows * p4 > zrow) {
             if (tid == 0 && a.error_flag) atomicOr(a.error_flag, 2);
             return;
         }
     }
+    RT_STAMP(0);
     // ---- fill the bottom level: every thread issues all its global loads
     // before the first LDS write (one HBM round trip per item, not per element)
     {
@@ -289,12 +295,14 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
         int rem = total - tid;
         asm volatile("" : "+v"(r), "+v"(col), "+v"(rem));
         const int dr = kConeBlock / p, dc = kConeBlock - (kConeBlock / p) * p;
+        int lo[kRegsPerThread];
 #pragma unroll
         for (int k = 0; k < kRegsPerThread; ++k) {
             if (rem > k * kConeBlock) {
                 const uint64_t off = tile ? (uint64_t)desc[r].x * p + col : (uint64_t)(k * kConeBlock + tid);
                 v[k] = base[off];
             }
+            lo[k] = r * p4 + col;                         // padded LDS row layout
             r += dr;
             col += dc;
             if (col >= p) {
@@ -304,15 +312,16 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
         }
 #pragma unroll
         for (int k = 0; k < kRegsPerThread; ++k)
-            if (rem > k * kConeBlock) data[k * kConeBlock + tid] = v[k];
+            if (rem > k * kConeBlock) data[lo[k]] = v[k];
     }
     __syncthreads();
+    RT_STAMP(1);
 
-    // ---- merge levels, deepest first
-    for (int l = L - 1; l >= 0; --l) {
-        if (l == L - 1) {
-            for (int i = tid; i < p; i += kConeBlock) data[zrow + i] = -0.0f;
-        }
+    // ---- merge levels, deepest first.  Two barriers per level: the row
+    // descriptors of level l-1 are built while level l is written back.
+    // Descriptor of output row r of level l: (head row | tail row << 16) in
+    // floats, and the roll shift (transforms.hpp:13-27).
+    auto build_desc = [&](int l) {
         const int orows = tile ? lv_rows[l] : (int)it.node_size;
         for (int r = tid; r < orows; r += kConeBlock) {
             int hrow, trow = -1, shift = 0;
@@ -352,57 +361,71 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
                     shift = (s - t) % p;
                 }
             }
-            const int ho = hrow * p;
-            const int to = trow < 0 ? zrow : trow * p;
+            const int ho = hrow * p4;
+            const int to = trow < 0 ? zrow : trow * p4;
             desc[r] = make_int2(ho | (to << 16), shift);
         }
-        __syncthreads();
-        const int total = orows * p;
-        float v[kRegsPerThread];
-        // (row, col) of element e = k * kConeBlock + tid, advanced incrementally
-        int r = div_rows(tid, p, inv_p);
-        int col = tid - r * p;
-        // opaque per level: stops LICM from hoisting all per-element indices
-        // out of the level loop (which spills the register file)
-        asm volatile("" : "+v"(r), "+v"(col));
-        const int dr = kConeBlock / p, dc = kConeBlock - (kConeBlock / p) * p;
+    };
+    for (int i = tid; i < p4; i += kConeBlock) data[zrow + i] = -0.0f;
+    if (L > 0) build_desc(L - 1);
+    __syncthreads();
+    RT_STAMP(2);
+    for (int l = L - 1; l >= 0; --l) {
+        const int orows = tile ? lv_rows[l] : (int)it.node_size;
+        // Quads: lane-owned groups of 4 consecutive phase bins of one row (rows
+        // are padded to p4).  H is one aligned ds_read_b128, the rolled T four
+        // ds_read_b32, the result one ds_write_b128; pad columns carry garbage
+        // that only ever flows into pad columns.
+        const int totalq = orows * qpr;
+        float4 v[kQuadsPerThread];
+        int r = div_rows(tid, qpr, 1.0f / (float)qpr);
+        int q = tid - r * qpr;
+        // opaque per level: stops LICM from hoisting all per-quad indices out
+        // of the level loop (which spills the register file)
+        asm volatile("" : "+v"(r), "+v"(q));
+        const int dr = kConeBlock / qpr, dq = kConeBlock - (kConeBlock / qpr) * qpr;
         const int last_row = orows - 1;
-        // Branch-free body, groups of kMergeGroup elements per thread: every
-        // group issues all its descriptor reads, then all its data reads, so the
-        // LDS latency is paid once per group.  Elements past the end of the
-        // level read a clamped (valid) row and are not written back.
 #pragma unroll
-        for (int g = 0; g < kRegsPerThread; g += kMergeGroup) {
-            if (g * kConeBlock < total) {          // uniform: whole group inactive otherwise
+        for (int g = 0; g < kQuadsPerThread; g += kMergeGroup) {
+            if (g * kConeBlock < totalq) {         // uniform: whole group inactive otherwise
 #pragma unroll
-                for (int j = 0; j < kMergeGroup && g + j < kRegsPerThread; ++j) {
+                for (int j = 0; j < kMergeGroup && g + j < kQuadsPerThread; ++j) {
                     const int2 d = desc[min(r, last_row)];
                     const int ho = d.x & 0xFFFF;
                     const int to = (int)((unsigned)d.x >> 16);
-                    int c2 = col + d.y;
+                    const int col = q << 2;
+                    const float4 hv = data4[(ho + col) >> 2];   // ho, col multiples of 4
+                    int c0 = col + d.y;
+                    c0 = c0 >= p ? c0 - p : c0;
+                    int c1 = c0 + 1, c2 = c0 + 2, c3 = c0 + 3;
+                    c1 = c1 >= p ? c1 - p : c1;
                     c2 = c2 >= p ? c2 - p : c2;
+                    c3 = c3 >= p ? c3 - p : c3;
                     // carried rows point `to` at the -0.0 row: x + (-0.0) == x exactly
-                    v[g + j] = __fadd_rn(data[ho + col], data[to + c2]);
+                    v[g + j] = make_float4(__fadd_rn(hv.x, data[to + c0]), __fadd_rn(hv.y, data[to + c1]),
+                                           __fadd_rn(hv.z, data[to + c2]), __fadd_rn(hv.w, data[to + c3]));
                     r += dr;
-                    col += dc;
-                    const bool wrap = col >= p;
-                    col = wrap ? col - p : col;
+                    q += dq;
+                    const bool wrap = q >= qpr;
+                    q = wrap ? q - qpr : q;
                     r = wrap ? r + 1 : r;
                 }
             }
         }
         __syncthreads();
 #pragma unroll
-        for (int g = 0; g < kRegsPerThread; g += kMergeGroup) {
-            if (g * kConeBlock < total) {
+        for (int g = 0; g < kQuadsPerThread; g += kMergeGroup) {
+            if (g * kConeBlock < totalq) {
 #pragma unroll
-                for (int j = 0; j < kMergeGroup && g + j < kRegsPerThread; ++j) {
-                    const int e = (g + j) * kConeBlock + tid;
-                    if (e < total) data[e] = v[g + j];
+                for (int j = 0; j < kMergeGroup && g + j < kQuadsPerThread; ++j) {
+                    const int qi = (g + j) * kConeBlock + tid;
+                    if (qi < totalq) data4[qi] = v[g + j];
                 }
             }
         }
+        if (l > 0) build_desc(l - 1);
         __syncthreads();
+        RT_STAMP(3);
         nrows = orows;
     }
 
@@ -412,58 +435,167 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
                      (uint64_t)(it.node_start + it.s0) * p;
         const int rem = nrows * p - tid;
         float v[kRegsPerThread];
+        int r = div_rows(tid, p, inv_p);
+        int col = tid - r * p;
+        asm volatile("" : "+v"(r), "+v"(col));
+        const int dr = kConeBlock / p, dc = kConeBlock - (kConeBlock / p) * p;
 #pragma unroll
-        for (int k = 0; k < kRegsPerThread; ++k)
-            if (rem > k * kConeBlock) v[k] = data[k * kConeBlock + tid];
+        for (int k = 0; k < kRegsPerThread; ++k) {
+            if (rem > k * kConeBlock) v[k] = data[r * p4 + col];
+            r += dr;
+            col += dc;
+            if (col >= p) {
+                col -= p;
+                ++r;
+            }
+        }
 #pragma unroll
         for (int k = 0; k < kRegsPerThread; ++k)
             if (rem > k * kConeBlock) dst[k * kConeBlock + tid] = v[k];
+        RT_STAMP(4);
+#ifdef RT_STAMPS
+        if (tid == 0) atomicAdd(&a.stamps[7], 1ull);
+#endif
         return;
     }
 
     // ---- fused boxcar S/N epilogue (snr.hpp:37-65) on the root's rows s < rows_eval
     const int nev = (int)min((int64_t)nrows, (int64_t)X.rows_eval - (int64_t)it.s0);
     if (nev <= 0) return;
-    const int c = (p + 63) >> 6;
-    const int j0 = min(lane * c, p);
-    const int j1 = min(j0 + c, p);
+    // G lanes per row (G in 8..64, the smallest with ceil(p/G) <= kSnrChunk),
+    // each lane a chunk of c <= kSnrChunk columns held in registers; c is odd so
+    // the G chunks of a row hit distinct LDS banks.  fp64 prefix: sequential in
+    // the chunk + log2(G)-step segmented scan (kernels.hpp:73-86).
+    int G = 8;
+    while (G < 64 && ((((p + G - 1) / G) | 1) > kSnrChunk)) G <<= 1;
+    int c = (p + G - 1) / G;
+    if (c < kSnrChunk) c |= 1;
+    const int g = lane & (G - 1);
+    const int j0 = min(g * c, p);
+    const int cnt = min(j0 + c, p) - j0;          // columns of this lane (may be 0)
     const int owner = (p - 1) / c;
-    for (int r = wave; r < nev; r += kConeBlock / 64) {
-        float* row = data + r * p;
-        double part = 0.0;
-        for (int j = j0; j < j1; ++j) part += (double)row[j];
-        const double incl = wave_incl_scan(part, lane);
-        double acc = __shfl_up(incl, 1, 64);
-        if (lane == 0) acc = 0.0;
-        for (int j = j0; j < j1; ++j) {
-            acc += (double)row[j];
-            row[j] = (float)acc;    // circular_prefix_sum, kernels.hpp:73-86 (fp64 accumulator)
-        }
-        const float sum = __shfl((float)acc, owner, 64);
-        if (lane == 0) desc[r].x = __float_as_int(sum);
-    }
-    __syncthreads();
+    const int rows_per_pass = kConeBlock / G;
     const uint32_t nw = a.num_widths;
     float* snr = a.snr + trial * a.snr_stride + (X.snr_row + it.s0) * (uint64_t)nw;
-    for (int r = wave; r < nev; r += kConeBlock / 64) {
-        const float* row = data + r * p;
-        const float sum = __int_as_float(desc[r].x);
-        for (uint32_t iw = 0; iw < nw; ++iw) {
-            const int w = (int)a.widths[iw];
-            float dmax = -INFINITY;
-            for (int i = j0; i < j1; ++i) {
-                const int k = i + w;
-                const float ck = k < p ? row[k] : __fadd_rn(row[k - p], sum);
-                dmax = fmaxf(dmax, __fsub_rn(ck, row[i]));
+    if (c <= kSnrChunk) {
+        for (int base = 0; base < nev; base += rows_per_pass) {
+            const int r = base + (tid / G);
+            const bool active = r < nev;
+            float* row = data + min(r, nev - 1) * p4 + j0;
+            const int last = max(cnt - 1, 0);
+            float cp[kSnrChunk];
+            // branch-free: every lane issues all kSnrChunk reads (clamped to its
+            // chunk), values past the chunk are masked
+#pragma unroll
+            for (int i = 0; i < kSnrChunk; ++i) {
+                const float x = row[min(i, last)];
+                cp[i] = i < cnt ? x : 0.0f;
             }
-            dmax = wave_max(dmax);
-            if (lane == 0) {
-                const float h = sqrtf((float)(p - w) / (float)(p * w));
-                const float b = (float)w / (float)(p - w) * h;
-                snr[(uint64_t)r * nw + iw] = ((h + b) * dmax - b * sum) / X.stdnoise;
+            double part = 0.0;
+#pragma unroll
+            for (int i = 0; i < kSnrChunk; ++i) {
+                const double t = part + (double)cp[i];
+                part = i < cnt ? t : part;
+            }
+            double incl = part;
+            for (int d = 1; d < G; d <<= 1) {
+                const double y = __shfl_up(incl, d, G);
+                if (g >= d) incl += y;
+            }
+            double acc = __shfl_up(incl, 1, G);
+            if (g == 0) acc = 0.0;
+#pragma unroll
+            for (int i = 0; i < kSnrChunk; ++i) {
+                const double t = acc + (double)cp[i];
+                acc = i < cnt ? t : acc;
+                cp[i] = (float)acc;
+            }
+            const float sum = __shfl((float)acc, owner, G);
+            if (active) {
+#pragma unroll
+                for (int i = 0; i < kSnrChunk; ++i)
+                    if (i < cnt) row[i] = cp[i];
+            }
+            __syncthreads();                      // prefix rows visible to all lanes
+            const float* crow = data + min(r, nev - 1) * p4;
+            for (uint32_t iw = 0; iw < nw; ++iw) {
+                const int w = wl[iw];
+                float dmax = -INFINITY;
+                constexpr int kB = 11;                    // reads in flight per batch
+                static_assert(kSnrChunk % kB == 0, "batching");
+#pragma unroll
+                for (int b0 = 0; b0 < kSnrChunk; b0 += kB) {
+                    float lv[kB];
+#pragma unroll
+                    for (int t = 0; t < kB; ++t) {
+                        const int k = j0 + min(b0 + t, last) + w;
+                        lv[t] = crow[k >= p ? k - p : k];
+                    }
+#pragma unroll
+                    for (int t = 0; t < kB; ++t) {
+                        const int i = b0 + t;
+                        const bool wrap = j0 + min(i, last) + w >= p;
+                        const float ck = wrap ? __fadd_rn(lv[t], sum) : lv[t];
+                        const float d = __fsub_rn(ck, cp[i]);
+                        dmax = (i < cnt && d > dmax) ? d : dmax;  // diff_max, kernels.hpp:50-60
+                    }
+                }
+                for (int o = G >> 1; o > 0; o >>= 1) {
+                    const float y = __shfl_xor(dmax, o, G);
+                    dmax = y > dmax ? y : dmax;
+                }
+                if (active && g == 0) {
+                    const float h = sqrtf((float)(p - w) / (float)(p * w));
+                    const float b = (float)w / (float)(p - w) * h;
+                    snr[(uint64_t)r * nw + iw] = ((h + b) * dmax - b * sum) / X.stdnoise;
+                }
             }
         }
+    } else {
+        // very wide rows (p > 64 * kSnrChunk): one wave per row, chunks from LDS
+        for (int base = 0; base < nev; base += kConeBlock / 64) {
+            const int r = base + wave;
+            const bool active = r < nev;
+            float* row = data + min(r, nev - 1) * p4;
+            double part = 0.0;
+            for (int j = j0; j < j0 + cnt; ++j) part += (double)row[j];
+            double incl = part;
+            for (int d = 1; d < 64; d <<= 1) {
+                const double y = __shfl_up(incl, d, 64);
+                if (g >= d) incl += y;
+            }
+            double acc = __shfl_up(incl, 1, 64);
+            if (g == 0) acc = 0.0;
+            __syncthreads();
+            if (active)
+                for (int j = j0; j < j0 + cnt; ++j) {
+                    acc += (double)row[j];
+                    row[j] = (float)acc;
+                }
+            const float sum = __shfl((float)acc, owner, 64);
+            __syncthreads();
+            for (uint32_t iw = 0; iw < nw; ++iw) {
+                const int w = (int)a.widths[iw];
+                float dmax = -INFINITY;
+                for (int i = j0; i < j0 + cnt; ++i) {
+                    const int k = i + w;
+                    const float ck = k < p ? row[k] : __fadd_rn(row[k - p], sum);
+                    dmax = fmaxf(dmax, __fsub_rn(ck, row[i]));
+                }
+                for (int o = 32; o > 0; o >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, o, 64));
+                if (active && g == 0) {
+                    const float h = sqrtf((float)(p - w) / (float)(p * w));
+                    const float b = (float)w / (float)(p - w) * h;
+                    snr[(uint64_t)r * nw + iw] = ((h + b) * dmax - b * sum) / X.stdnoise;
+                }
+            }
+            __syncthreads();
+        }
     }
+    RT_STAMP(5);
+#ifdef RT_STAMPS
+    if (tid == 0) atomicAdd(&a.stamps[7], 1ull);
+#endif
 }
 
 hipError_t launch_cone(const ConeArgs& args, uint32_t batch, hipStream_t s)

@@ -128,11 +128,12 @@ ConeNeed cone_need(uint32_t node_size, uint32_t s0, uint32_t s1, int levels, uin
     struct R { uint32_t size, lo, hi; };
     std::vector<R> cur{{node_size, s0, s1 - 1}}, nxt;
     ConeNeed need;
+    const int stride = lds_row_stride(p);
     auto account = [&](const std::vector<R>& lv) {
         int rows = 0, floats = 0;
         for (const R& r : lv) {
             rows += (int)(r.hi - r.lo + 1);
-            floats += (int)((r.hi - r.lo + 1) * p + 3);
+            floats += (int)(r.hi - r.lo + 1) * stride;
         }
         need.max_rows = std::max(need.max_rows, rows);
         need.max_floats = std::max(need.max_floats, floats);
