@@ -28,9 +28,9 @@
 namespace rt {
 
 // ---- cone kernel geometry (gfx950: 160 KiB LDS per CU, one workgroup per CU)
-constexpr int kConeBlock = 1024;            // 16 waves
-constexpr int kLdsDataFloats = 34816;       // 136 KiB level buffer
-constexpr int kMaxRows = 1024;              // rows per level held in LDS (row descriptors)
+constexpr int kConeBlock = 512;             // 8 waves, 2 workgroups per CU
+constexpr int kLdsDataFloats = 16384;       // 64 KiB level buffer
+constexpr int kMaxRows = 512;               // rows per level held in LDS (row descriptors)
 constexpr int kMaxTileLevels = 6;           // L for tile items
 constexpr int kMaxRanges = (1 << (kMaxTileLevels + 1)) - 1;
 constexpr int kMaxWholeLevels = 11;         // ceil(log2(kMaxRows)) + 1
