@@ -40,6 +40,10 @@ constexpr int kSnrChunk = 33;             // S/N epilogue: columns per lane held
 constexpr int kMergeGroup = 8;             // elements per thread with LDS reads in flight together
 
 constexpr int kQuadsPerThread = (kLdsDataFloats / 4 + kConeBlock - 1) / kConeBlock;
+// float4 chunks per thread of the fill/store phases: a level of n rows of
+// stride p4 spans at most n*p4/4 + n aligned chunks (one extra per row for
+// misalignment), n*p4 < kLdsDataFloats and n <= kMaxRows.
+constexpr int kFillChunks = (kLdsDataFloats / 4 + kMaxRows + kConeBlock - 1) / kConeBlock;
 
 // LDS rows are padded to a multiple of 4 floats (16-byte aligned rows) so the
 // merge can move 4 phase bins per lane with ds_read_b128 / ds_write_b128.

@@ -284,35 +284,48 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
         }
     }
     RT_STAMP(0);
-    // ---- fill the bottom level: every thread issues all its global loads
-    // before the first LDS write (one HBM round trip per item, not per element)
+    // ---- fill the bottom level with 16-byte loads.  Row r is global row
+    // grow(r), floats [grow*p, grow*p + p) of a 16-byte aligned buffer, covered
+    // by at most nch aligned float4 chunks: chunk c holds elements
+    // e = 4c + j - al (al = grow*p & 3), kept when 0 <= e < p.  Every thread
+    // issues all its loads before the first LDS write.
     {
-        const int total = nrows * p;
-        const float* base = tile ? src : src + (uint64_t)it.node_start * p;
-        float v[kRegsPerThread];
-        int r = div_rows(tid, p, inv_p);
-        int col = tid - r * p;
-        int rem = total - tid;
-        asm volatile("" : "+v"(r), "+v"(col), "+v"(rem));
-        const int dr = kConeBlock / p, dc = kConeBlock - (kConeBlock / p) * p;
-        int lo[kRegsPerThread];
+        const int amax = (p & 3) == 0 ? 0 : ((p & 1) == 0 ? 2 : 3);
+        const int nch = (p + amax + 3) >> 2;                 // chunks per row (upper bound)
+        const int totalc = nrows * nch;
+        float4 v[kFillChunks];
+        int lo[kFillChunks], e0[kFillChunks];
+        int r = div_rows(tid, nch, 1.0f / (float)nch);
+        int c = tid - r * nch;
+        asm volatile("" : "+v"(r), "+v"(c));
+        const int dr = kConeBlock / nch, dc = kConeBlock - (kConeBlock / nch) * nch;
 #pragma unroll
-        for (int k = 0; k < kRegsPerThread; ++k) {
-            if (rem > k * kConeBlock) {
-                const uint64_t off = tile ? (uint64_t)desc[r].x * p + col : (uint64_t)(k * kConeBlock + tid);
-                v[k] = base[off];
-            }
-            lo[k] = r * p4 + col;                         // padded LDS row layout
+        for (int k = 0; k < kFillChunks; ++k) {
+            const int rr = min(r, nrows - 1);
+            const int grow = tile ? desc[rr].x : (int)it.node_start + rr;
+            const uint64_t g = (uint64_t)grow * p;
+            const int al = (int)(g & 3);
+            int e = 4 * c - al;
+            if (k * kConeBlock + tid >= totalc) e = p;       // inactive chunk
+            if (e < p) v[k] = *reinterpret_cast<const float4*>(src + (g - al) + 4 * c);
+            lo[k] = rr * p4;
+            e0[k] = e;
             r += dr;
-            col += dc;
-            if (col >= p) {
-                col -= p;
+            c += dc;
+            if (c >= nch) {
+                c -= nch;
                 ++r;
             }
         }
 #pragma unroll
-        for (int k = 0; k < kRegsPerThread; ++k)
-            if (rem > k * kConeBlock) data[lo[k]] = v[k];
+        for (int k = 0; k < kFillChunks; ++k) {
+            const int e = e0[k];
+            float* row = data + lo[k];
+            if ((unsigned)e < (unsigned)p) row[e] = v[k].x;
+            if ((unsigned)(e + 1) < (unsigned)p) row[e + 1] = v[k].y;
+            if ((unsigned)(e + 2) < (unsigned)p) row[e + 2] = v[k].z;
+            if ((unsigned)(e + 3) < (unsigned)p) row[e + 3] = v[k].w;
+        }
     }
     __syncthreads();
     RT_STAMP(1);
@@ -429,19 +442,46 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
         nrows = orows;
     }
 
-    // ---- output: tile rows [s0, s0 + nrows) of the node
+    // ---- output: tile rows [s0, s0 + nrows) of the node, one contiguous
+    // global segment written in aligned float4 chunks (segment-end chunks
+    // element-wise).  Chunk c holds segment elements e = 4c + j - al.
     if (it.dst != kSelSnr) {
-        float* dst = (it.dst == kSelPing ? a.ping : a.pong) + trial * a.buf_stride + X.buf_off +
-                     (uint64_t)(it.node_start + it.s0) * p;
-        const int rem = nrows * p - tid;
-        float v[kRegsPerThread];
-        int r = div_rows(tid, p, inv_p);
-        int col = tid - r * p;
+        const uint64_t g0 = (uint64_t)(it.node_start + it.s0) * p;
+        const int al = (int)(g0 & 3);
+        float* dst = (it.dst == kSelPing ? a.ping : a.pong) + trial * a.buf_stride + X.buf_off + (g0 - al);
+        const int total = nrows * p;
+        const int totalc = (total + al + 3) >> 2;
+        float4 v[kFillChunks];
+        // (row, col) of element e = 4*tid - al, stepped by 4*kConeBlock per chunk
+        int e = 4 * tid - al;
+        int r = e < 0 ? -1 : div_rows(e, p, inv_p);
+        int col = e - r * p;
         asm volatile("" : "+v"(r), "+v"(col));
-        const int dr = kConeBlock / p, dc = kConeBlock - (kConeBlock / p) * p;
+        constexpr int kStep = 4 * kConeBlock;
+        const int dr = kStep / p, dc = kStep - (kStep / p) * p;
 #pragma unroll
-        for (int k = 0; k < kRegsPerThread; ++k) {
-            if (rem > k * kConeBlock) v[k] = data[r * p4 + col];
+        for (int k = 0; k < kFillChunks; ++k) {
+            if (k * kConeBlock + tid < totalc) {
+                float x[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    int cj = col + j, rj = r;
+                    if (cj >= p) {
+                        cj -= p;
+                        ++rj;
+                    }
+                    if (p < 4) {                 // uniform: several wraps inside a chunk
+                        while (cj >= p) {
+                            cj -= p;
+                            ++rj;
+                        }
+                    }
+                    const int ej = e + j;
+                    x[j] = data[((unsigned)ej < (unsigned)total) ? rj * p4 + cj : 0];
+                }
+                v[k] = make_float4(x[0], x[1], x[2], x[3]);
+            }
+            e += kStep;
             r += dr;
             col += dc;
             if (col >= p) {
@@ -450,8 +490,20 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
             }
         }
 #pragma unroll
-        for (int k = 0; k < kRegsPerThread; ++k)
-            if (rem > k * kConeBlock) dst[k * kConeBlock + tid] = v[k];
+        for (int k = 0; k < kFillChunks; ++k) {
+            const int ci = k * kConeBlock + tid;
+            if (ci < totalc) {
+                const int eb = 4 * ci - al;
+                if (eb >= 0 && eb + 3 < total) {
+                    *reinterpret_cast<float4*>(dst + 4 * ci) = v[k];
+                } else {
+                    if ((unsigned)eb < (unsigned)total) dst[4 * ci] = v[k].x;
+                    if ((unsigned)(eb + 1) < (unsigned)total) dst[4 * ci + 1] = v[k].y;
+                    if ((unsigned)(eb + 2) < (unsigned)total) dst[4 * ci + 2] = v[k].z;
+                    if ((unsigned)(eb + 3) < (unsigned)total) dst[4 * ci + 3] = v[k].w;
+                }
+            }
+        }
         RT_STAMP(4);
 #ifdef RT_STAMPS
         if (tid == 0) atomicAdd(&a.stamps[7], 1ull);

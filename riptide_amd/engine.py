@@ -95,10 +95,12 @@ class PeriodogramPlan:
                                         _stream_handle(stream)))
         return out[0] if squeeze else out
 
-    def __del__(self):
+    def __del__(self, _destroy=_L.rt_plan_destroy):
+        # the default argument keeps the function alive through interpreter
+        # shutdown, when module globals may already be cleared
         h = getattr(self, "_h", None)
         if h is not None and h.value:
-            _L.rt_plan_destroy(h)
+            _destroy(h)
             self._h = None
 
 
