@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -114,6 +115,17 @@ void sync(hipStream_t s) { ck(hipStreamSynchronize(s), "hipStreamSynchronize"); 
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// Per-trial scratch budget (floats per ping/pong buffer) of one transform group.
+// Tuning knob for experiments: RIPTIDE_AMD_SCRATCH_MFLOATS (millions of floats).
+uint64_t scratch_budget_floats()
+{
+    if (const char* e = std::getenv("RIPTIDE_AMD_SCRATCH_MFLOATS")) {
+        const double v = std::atof(e);
+        if (v > 0) return (uint64_t)(v * 1e6);
+    }
+    return 32ull << 20;
+}
+
 // ---- profiling of cone / downsample launches
 struct ProfRec {
     hipEvent_t a, b;
@@ -138,26 +150,41 @@ struct Profiler {
 
 // ---- a compiled plan resident on one device
 struct DevicePlan {
-    std::vector<FfaXform> xf;
     ExecPlan ex;
-    FfaXform* d_xf = nullptr;
-    ConeItem* d_items = nullptr;
+    UnitDesc* d_units = nullptr;
     int device = 0;
     ~DevicePlan()
     {
-        if (d_xf) (void)hipFree(d_xf);
-        if (d_items) (void)hipFree(d_items);
+        if (d_units) (void)hipFree(d_units);
     }
     void upload()
     {
         ck(hipGetDevice(&device), "hipGetDevice");
-        ck(hipMalloc(&d_xf, std::max<size_t>(1, ex.xf.size()) * sizeof(FfaXform)), "hipMalloc");
-        ck(hipMalloc(&d_items, std::max<size_t>(1, ex.items.size()) * sizeof(ConeItem)), "hipMalloc");
-        if (!ex.xf.empty())
-            ck(hipMemcpy(d_xf, ex.xf.data(), ex.xf.size() * sizeof(FfaXform), hipMemcpyHostToDevice), "upload xf");
-        if (!ex.items.empty())
-            ck(hipMemcpy(d_items, ex.items.data(), ex.items.size() * sizeof(ConeItem), hipMemcpyHostToDevice),
-               "upload items");
+        std::vector<UnitDesc> u(ex.items.size());
+        for (size_t i = 0; i < u.size(); ++i) {
+            const ConeItem& it = ex.items[i];
+            const FfaXform& X = ex.xf[it.xform];
+            UnitDesc d{};
+            d.node_start = it.node_start;
+            d.node_size = it.node_size;
+            d.s0 = it.s0;
+            d.s1 = it.s1;
+            d.p = X.p;
+            d.m = X.m;
+            d.rows_eval = X.rows_eval;
+            d.stdnoise = X.stdnoise;
+            d.src_off = X.src_off;
+            d.buf_off = X.buf_off;
+            d.snr_row = X.snr_row;
+            d.levels = it.levels;
+            d.mode = it.mode;
+            d.src = it.src;
+            d.dst = it.dst;
+            u[i] = d;
+        }
+        ck(hipMalloc(&d_units, std::max<size_t>(1, u.size()) * sizeof(UnitDesc)), "hipMalloc");
+        if (!u.empty())
+            ck(hipMemcpy(d_units, u.data(), u.size() * sizeof(UnitDesc), hipMemcpyHostToDevice), "upload units");
     }
 };
 
@@ -167,11 +194,17 @@ unsigned long long* g_stamps = nullptr;
 // Run all cone launches of an exec plan.
 void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStream_t s)
 {
-    a.xf = P.d_xf;
     a.stamps = g_stamps;
-    for (const Launch& L : P.ex.launches) {
-        a.items = P.d_items + L.first;
+    a.batch = batch;
+    a.flags = kConeAllFeatures;
+    if (const char* e = std::getenv("RIPTIDE_AMD_CONE_FLAGS")) a.flags = (uint32_t)std::strtoul(e, nullptr, 0);
+    for (size_t li = 0; li < P.ex.launches.size(); ++li) {
+        const Launch& L = P.ex.launches[li];
+        a.items = P.d_units + L.first;
         a.num_items = L.count;
+        const uint64_t units = (uint64_t)L.count * batch;   // one workgroup per (item, trial)
+        if (units > 0x7FFFFFFFull) throw std::invalid_argument("too many cone work units in one launch");
+        const uint32_t grid = (uint32_t)units;
         ProfRec r{};
         if (g_prof.on) {
             r.a = g_prof.ev();
@@ -180,7 +213,7 @@ void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStrea
             r.moved = L.moved_bytes * batch;
             ck(hipEventRecord(r.a, s), "hipEventRecord");
         }
-        ck(launch_cone(a, batch, s), "cone_kernel");
+        ck(launch_cone(a, grid, L.smax, s), "cone_kernel");
         if (g_prof.on) {
             ck(hipEventRecord(r.b, s), "hipEventRecord");
             g_prof.rec[0].push_back(r);
@@ -256,12 +289,14 @@ struct rt_plan {
     PgramPlan pg;
     DevicePlan dp;
     std::vector<uint32_t> widths;
+    uint32_t* d_widths = nullptr;
     std::vector<DsRung> rungs;
     DsRung* d_rungs = nullptr;
     uint32_t ds_blocks = 0;
     ~rt_plan()
     {
         if (d_rungs) (void)hipFree(d_rungs);
+        if (d_widths) (void)hipFree(d_widths);
     }
 };
 
@@ -286,6 +321,9 @@ rt_plan* make_plan(size_t size, double tsamp, const uint64_t* widths, size_t nw,
     try {
         build_pgram_plan(prm, P->pg);
         P->widths.assign(widths, widths + nw);
+        ck(hipMalloc(&P->d_widths, std::max<size_t>(1, nw) * sizeof(uint32_t)), "hipMalloc");
+        if (nw)
+            ck(hipMemcpy(P->d_widths, P->widths.data(), nw * sizeof(uint32_t), hipMemcpyHostToDevice), "upload widths");
         std::vector<FfaXform> xf;
         for (const Step& s : P->pg.steps) {
             if (!s.rows_eval) continue;   // nothing of this transform reaches the output
@@ -300,7 +338,7 @@ rt_plan* make_plan(size_t size, double tsamp, const uint64_t* widths, size_t nw,
             xf.push_back(X);
         }
         // scratch budget per ping/pong buffer and trial: 32 M floats (128 MiB)
-        build_exec_plan(xf, true, (uint32_t)nw, 32ull << 20, P->dp.ex);
+        build_exec_plan(xf, true, (uint32_t)nw, scratch_budget_floats(), P->dp.ex);
         P->dp.upload();
         // downsample ladder over the rungs that feed at least one transform
         std::vector<bool> used(P->pg.rungs.size(), false);
@@ -370,7 +408,7 @@ void run_periodogram(const rt_plan* P, const float* d_data, size_t batch, size_t
     }
     ConeArgs a{};
     a.num_widths = (uint32_t)P->widths.size();
-    for (size_t i = 0; i < P->widths.size(); ++i) a.widths[i] = P->widths[i];
+    a.widths = P->d_widths;
     a.leaves = leaves;
     a.leaves_stride = P->pg.leaf_floats;
     a.ping = ping;
@@ -780,7 +818,7 @@ int rt_schedule_check(size_t size, double tsamp, size_t nw, double pmin, double 
             xf.push_back(X);
         }
         ExecPlan ex;
-        build_exec_plan(xf, true, (uint32_t)nw, 32ull << 20, ex);
+        build_exec_plan(xf, true, (uint32_t)nw, scratch_budget_floats(), ex);
         // invariants: within every launch, each transform's items write disjoint
         // row ranges, every item fits the LDS budget, and the last pass of every
         // transform covers rows [0, m) exactly once.

@@ -27,35 +27,58 @@
 
 namespace rt {
 
-// ---- cone kernel geometry (gfx950: 160 KiB LDS per CU, one workgroup per CU)
-constexpr int kConeBlock = 512;             // 8 waves, 2 workgroups per CU
-constexpr int kLdsDataFloats = 16384;       // 64 KiB level buffer
-constexpr int kMaxRows = 512;               // rows per level held in LDS (row descriptors)
+// ---- cone kernel geometry (gfx950: 160 KiB LDS per CU).  512-thread
+// workgroups with ~77 KiB of LDS each, two per CU; the level buffer holds
+// dense rows (stride p).
+constexpr int kConeBlock = 512;             // 8 waves
+constexpr int kConeWaves = kConeBlock / 64;
+constexpr int kLdsDataFloats = 17408;       // 68 KiB level buffer
+constexpr int kLdsPadFloats = 128;          // slack read (never used) by the unused slots of the last row
+constexpr int kMaxRows = 512;               // rows per level (source-row table, descriptors)
+constexpr int kDescEntries = 1024;          // row-descriptor table (all levels of a unit)
 constexpr int kMaxTileLevels = 6;           // L for tile items
 constexpr int kMaxRanges = (1 << (kMaxTileLevels + 1)) - 1;
-constexpr int kMaxWholeLevels = 11;         // ceil(log2(kMaxRows)) + 1
-constexpr int kMaxWidths = 32;           // boxcar widths handled by the fused S/N epilogue
-constexpr int kRegsPerThread = (kLdsDataFloats + kConeBlock - 1) / kConeBlock;
-constexpr int kSnrChunk = 33;             // S/N epilogue: columns per lane held in registers
-constexpr int kMergeGroup = 8;             // elements per thread with LDS reads in flight together
-
-constexpr int kQuadsPerThread = (kLdsDataFloats / 4 + kConeBlock - 1) / kConeBlock;
-// float4 chunks per thread of the fill/store phases: a level of n rows of
-// stride p4 spans at most n*p4/4 + n aligned chunks (one extra per row for
-// misalignment), n*p4 < kLdsDataFloats and n <= kMaxRows.
+constexpr int kMaxWidths = 32;              // boxcar widths handled by the fused S/N epilogue
+constexpr int kSnrChunk = 17;               // S/N epilogue: columns per lane held in registers
+constexpr int kStageRegs = 45;              // merge: staged output values per lane (rows x slots)
+constexpr int kMaxSlots = 45;               // merge: 64-bin slots per row (p <= 2880)
+constexpr int kMaxRowsPerWave = 24;         // merge: staged rows per wave (SGPR descriptors per row)
+// float4 chunks per thread of the fill: a level of n rows spans at most
+// n*p/4 + n aligned chunks (one extra per row for misalignment), n*p <=
+// kLdsDataFloats and n <= kMaxRows.
 constexpr int kFillChunks = (kLdsDataFloats / 4 + kMaxRows + kConeBlock - 1) / kConeBlock;
 
-// LDS rows are padded to a multiple of 4 floats (16-byte aligned rows) so the
-// merge can move 4 phase bins per lane with ds_read_b128 / ds_write_b128.
-RT_HD inline int lds_row_stride(uint32_t p) { return (int)((p + 3) & ~3u); }
-
-// Row capacity of the LDS level buffer for p phase bins (one row is kept free
-// for the -0.0 row that carried leaves add).
-RT_HD inline int lds_row_capacity(uint32_t p)
+// Merge variant for rows of p phase bins: slots per row rounded up to an
+// instantiated width (1..5, 8, 16, 45); 0 if p is too wide for the LDS engine.
+RT_HD inline int merge_slots(uint32_t p)
 {
-    const int c = kLdsDataFloats / lds_row_stride(p) - 1;
+    const int s = (int)((p + 63) / 64);
+    if (s <= 5) return s < 1 ? 1 : s;
+    if (s <= 8) return 8;
+    if (s <= 16) return 16;
+    if (s <= kMaxSlots) return kMaxSlots;
+    return 0;
+}
+
+// Rows per wave the merge stages for a slot width (register budget).
+RT_HD constexpr int merge_rows_per_wave(int smax)
+{
+    return kStageRegs / smax < kMaxRowsPerWave ? kStageRegs / smax : kMaxRowsPerWave;
+}
+
+// Row capacity of one cone work unit for p phase bins run by the kernel
+// variant of slot width smax (>= merge_slots(p)): the level buffer, and the
+// register staging of a level (merge_rows_per_wave(smax) rows per wave).
+RT_HD inline int lds_row_capacity(uint32_t p, int smax)
+{
+    if (!smax || p == 0) return 0;
+    int c = kLdsDataFloats / (int)p;
+    const int stage = kConeWaves * merge_rows_per_wave(smax);
+    if (stage < c) c = stage;
     return c < kMaxRows ? c : kMaxRows;
 }
+
+RT_HD inline int lds_row_capacity(uint32_t p) { return lds_row_capacity(p, merge_slots(p)); }
 
 // One FFA transform of a plan ((rung, bins) step of periodogram.hpp:223-269).
 struct FfaXform {
@@ -72,6 +95,8 @@ struct FfaXform {
 static_assert(sizeof(FfaXform) == 48, "FfaXform layout");
 
 enum : uint8_t { kModeWhole = 0, kModeTile = 1 };
+// cone kernel feature bits (ConeArgs::flags)
+enum : uint32_t { kConeStoreFromRegs = 1u, kConeAllFeatures = 1u };
 enum : uint8_t { kSelLeaves = 0, kSelPing = 1, kSelPong = 2, kSelSnr = 3 };
 
 // One workgroup of one pass.
@@ -88,10 +113,21 @@ struct ConeItem {
 };
 static_assert(sizeof(ConeItem) == 28, "ConeItem layout");
 
+// Device form of one work item: the item and its transform in one 64-byte
+// record (a single scalar load per workgroup).
+struct UnitDesc {
+    uint32_t node_start, node_size, s0, s1;
+    uint32_t p, m, rows_eval;
+    float stdnoise;
+    uint64_t src_off, buf_off, snr_row;
+    uint8_t levels, mode, src, dst;
+    uint32_t pad;
+};
+static_assert(sizeof(UnitDesc) == 64, "UnitDesc layout");
+
 // Arguments of one cone-kernel launch.  Per-trial strides are in floats.
 struct ConeArgs {
-    const FfaXform* xf;
-    const ConeItem* items;
+    const UnitDesc* items;
     uint32_t num_items;
     uint32_t num_widths;
     const float* leaves;
@@ -101,9 +137,11 @@ struct ConeArgs {
     uint64_t buf_stride;
     float* snr;
     uint64_t snr_stride;
-    uint32_t widths[kMaxWidths];  // boxcar widths (bins)
+    const uint32_t* widths;  // boxcar widths (bins), device array of num_widths
     int* error_flag;      // set non-zero if a work item violates the LDS budget
     unsigned long long* stamps;   // RT_STAMPS diagnostic builds only: per-phase cycles
+    uint32_t batch;       // trials: work unit u = (item u / batch, trial u % batch)
+    uint32_t flags;       // kCone* feature bits (A/B experiments; default all set)
 };
 
 // Merge index of the FFA recursion (transforms.hpp:17-22): the reference build

@@ -88,32 +88,56 @@ hipError_t launch_downsample_ladder(const float* x, uint64_t n_in, uint64_t x_st
 // ---------------------------------------------------------------------------
 // Cone kernel
 // ---------------------------------------------------------------------------
-// One workgroup = one ConeItem: `levels` merge levels of the FFA recursion for
-// the rows of one tile (or one whole node), held entirely in LDS.
-//
-//   level l (0 = target node, `levels` = deepest) is a packed list of row
-//   ranges, one per node of the split tree at that depth that the tile depends
-//   on.  Each merge step computes level l from level l+1 into registers
-//   (flattened over rows x phase bins, 34 values per thread), then overwrites
-//   the LDS level buffer.  The merge is transforms.hpp:13-27:
-//       out[u][j] = H[h(u)][j] + T[t(u)][(j + u - t(u)) mod p]
-//
-// LDS: 136 KiB level buffer + 8 KiB row descriptors + range tree = ~147 KiB,
-// i.e. one workgroup per CU.
+// One workgroup (512 threads, 77 KiB of LDS: two workgroups per CU) per work
+// unit = one work item (UnitDesc) of one trial: `levels` merge levels of the FFA recursion
+// for the rows of one tile (or one whole node), held in LDS.  Phases:
+//   1. setup: unit view, rows per level, range tree of tile units (the
+//      planner guarantees 2^l ranges at cone level l)
+//   2. LDS-DMA of the bottom level (dense rows, row stride p); while it is in
+//      flight, the row descriptors of every level are built into a table
+//   3. merge levels, deepest first (transforms.hpp:13-27), one row per wave
+//      and one phase bin per lane:
+//          out[r][j] = H[h(r)][j] + T[t(r)][(j + shift(r)) mod p]
+//      The descriptor (head row, tail row, shift) is wave-uniform: lane i
+//      reads it for the wave's i-th row and the row loop takes it with
+//      v_readlane into SGPRs.  Bins j = lane + 64k use immediate offsets, so
+//      a 64-bin slot is one ds_read for H, one for T (consecutive lanes ->
+//      consecutive banks, conflict-free) and one ds_write.  A level's outputs
+//      are staged in registers between two barriers (in-place update).
+//   4. store the output rows (one contiguous segment), or the fused boxcar
+//      S/N epilogue (snr.hpp:37-65) when this is the transform's last pass.
+// The other workgroup on the CU overlaps its latency-bound phases (setup,
+// DMA wait, epilogue) with this one's LDS work.
 struct Range {          // rows [lo, hi] of one node of the split tree
     int size;           // rows of the node
     int lo, hi;         // node-local rows
     int start;          // first row of the node within the transform
     int base;           // first LDS row of this range in its level's packed layout
-    int child;          // index of the first child range (next level)
 };
 
-__device__ __forceinline__ int div_rows(int e, int p, float inv_p)
+
+// LDS-only workgroup barrier: orders LDS accesses without waiting for the
+// global loads (the next unit's prefetch) that are still in flight.
+__device__ __forceinline__ void lds_barrier()
 {
-    int r = (int)((float)e * inv_p);
-    if (r * p > e) --r;
-    else if ((r + 1) * p <= e) ++r;
-    return r;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ uint64_t uni64(uint64_t v)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+template <class T>
+__device__ __forceinline__ T* uni_ptr(T* p)
+{
+    return reinterpret_cast<T*>(uni64(reinterpret_cast<uint64_t>(p)));
 }
 
 __device__ __forceinline__ int wave_incl_scan_int(int v, int lane)
@@ -126,190 +150,204 @@ __device__ __forceinline__ int wave_incl_scan_int(int v, int lane)
     return v;
 }
 
-// Index of the last range in [first, first+count) whose base <= r.
-__device__ __forceinline__ int find_range(const Range* ranges, int first, int count, int r)
+// Wave-uniform view of one unit (scalar registers).
+struct UnitView {
+    int item, trial;
+    int node_start, node_size, s0, s1, levels, mode, src, dst;
+    int p, m, rows_eval;
+    uint64_t src_off, buf_off, snr_row;
+    float stdnoise;
+};
+
+// Per-unit metadata in LDS (double-buffered): the unit's view, rows per level
+// and the range tree of tile units.  Everything the merge and the epilogue of
+// a unit need is read from here, never from global memory, so no vmcnt wait
+// (which would also wait for the next unit's DMA) is needed after setup.
+struct UnitMeta {
+    UnitView view;
+    int nrows[kMaxTileLevels + 1];   // rows of every level (0 = output level)
+    Range ranges[kMaxRanges];        // tile units: level l holds 2^l ranges at (1 << l) - 1
+};
+
+__device__ __forceinline__ UnitView read_view(const UnitMeta& M)
 {
-    int lo = first, hi = first + count - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (ranges[mid].base <= r) lo = mid; else hi = mid - 1;
-    }
-    return lo;
+    UnitView v;
+    v.item = uni(M.view.item);
+    v.trial = uni(M.view.trial);
+    v.node_start = uni(M.view.node_start);
+    v.node_size = uni(M.view.node_size);
+    v.s0 = uni(M.view.s0);
+    v.s1 = uni(M.view.s1);
+    v.levels = uni(M.view.levels);
+    v.mode = uni(M.view.mode);
+    v.src = uni(M.view.src);
+    v.dst = uni(M.view.dst);
+    v.p = uni(M.view.p);
+    v.m = uni(M.view.m);
+    v.rows_eval = uni(M.view.rows_eval);
+    v.src_off = uni64(M.view.src_off);
+    v.buf_off = uni64(M.view.buf_off);
+    v.snr_row = uni64(M.view.snr_row);
+    v.stdnoise = __int_as_float(uni(__float_as_int(M.view.stdnoise)));
+    return v;
 }
 
-// Diagnostic build only (make stamps, -DRT_STAMPS): thread 0 adds the cycles of
-// each phase of the item to a.stamps[phase] (s_memtime; phases end at barriers).
-#ifdef RT_STAMPS
-#define RT_STAMP(i)                                                              \
-    do {                                                                         \
-        if (tid == 0) {                                                          \
-            const unsigned long long t_ = __builtin_amdgcn_s_memtime();          \
-            atomicAdd(&a.stamps[i], t_ - t_stamp);                               \
-            t_stamp = t_;                                                        \
-        }                                                                        \
-    } while (0)
-#else
-#define RT_STAMP(i) do { } while (0)
-#endif
-
-__global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
+__device__ __forceinline__ UnitView unit_view(const ConeArgs& a, int item, int trial)
 {
-#ifdef RT_STAMPS
-    unsigned long long t_stamp = __builtin_amdgcn_s_memtime();
-#endif
-    __shared__ float4 data4[kLdsDataFloats / 4];   // 16-byte aligned level buffer
-    float* const data = reinterpret_cast<float*>(data4);
-    __shared__ int2 desc[kMaxRows];
-    __shared__ Range ranges[kMaxRanges];
-    __shared__ int lv_first[kMaxTileLevels + 1];
-    __shared__ int lv_count[kMaxTileLevels + 1];
-    __shared__ int lv_rows[kMaxTileLevels + 1];
-    __shared__ int wl[kMaxWidths];           // boxcar widths, staged in LDS (DS ops wait by count)
+    UnitView v;
+    v.item = uni(item);
+    v.trial = uni(trial);
+    const UnitDesc d = a.items[v.item];
+    v.node_start = uni((int)d.node_start);
+    v.node_size = uni((int)d.node_size);
+    v.s0 = uni((int)d.s0);
+    v.s1 = uni((int)d.s1);
+    v.levels = uni((int)d.levels);
+    v.mode = uni((int)d.mode);
+    v.src = uni((int)d.src);
+    v.dst = uni((int)d.dst);
+    v.p = uni((int)d.p);
+    v.m = uni((int)d.m);
+    v.rows_eval = uni((int)d.rows_eval);
+    v.src_off = uni64(d.src_off);
+    v.buf_off = uni64(d.buf_off);
+    v.snr_row = uni64(d.snr_row);
+    v.stdnoise = __int_as_float(uni(__float_as_int(d.stdnoise)));
+    return v;
+}
 
-    const ConeItem it = a.items[blockIdx.x];
-    const FfaXform X = a.xf[it.xform];
-    const int p = (int)X.p;
-    const float inv_p = 1.0f / (float)p;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int L = it.levels;
-    const bool tile = it.mode == kModeTile;
-    const uint64_t trial = blockIdx.y;
-    if (tid < kMaxWidths) wl[tid] = (int)a.widths[tid];
-    const int p4 = lds_row_stride((uint32_t)p);          // LDS row stride (floats)
-    const int qpr = p4 >> 2;                               // quads per LDS row
-    // LDS row of -0.0f after the largest level the planner allows (lds_row_capacity)
-    const int zrow = (kLdsDataFloats / p4 - 1) * p4;
-
-    const float* src;
-    if (it.src == kSelLeaves) src = a.leaves + trial * a.leaves_stride + X.src_off;
-    else src = (it.src == kSelPing ? a.ping : a.pong) + trial * a.buf_stride + X.buf_off;
-
-    int nrows;
-    if (tile) {
-        // ---- dependency cone of the tile: top-down range tree, one lane per range (wave 0)
-        if (wave == 0) {
-            if (lane == 0) {
-                Range r0;
-                r0.size = (int)it.node_size;
-                r0.lo = (int)it.s0;
-                r0.hi = (int)it.s1 - 1;
-                r0.start = (int)it.node_start;
-                r0.base = 0;
-                r0.child = 0;
-                ranges[0] = r0;
-                lv_first[0] = 0;
-                lv_count[0] = 1;
-                lv_rows[0] = r0.hi - r0.lo + 1;
+// Metadata of unit u into M (+ the source-row table of its bottom level).
+// Every thread calls it; it ends with a barrier.
+__device__ __forceinline__ void setup_unit(const ConeArgs& a, int u, UnitMeta& M, int* src_row, int tid)
+{
+    const int lane = tid & 63, wave = tid >> 6;
+    const int batch = (int)a.batch;
+    const UnitView U = unit_view(a, u / batch, u % batch);
+    if (tid == 0) M.view = U;
+    const int L = U.levels;
+    if (U.mode == kModeTile) {
+        // level l (wave l): lane i walks the head/tail path i (MSB first) from
+        // the tile; the planner guarantees every node above the bottom level
+        // has >= 2 rows, so level l has exactly 2^l ranges
+        if (wave <= L) {
+            const int l = wave;
+            const int nr = 1 << l;
+            Range R{0, 0, -1, 0, 0};
+            if (lane < nr) {
+                uint32_t size = (uint32_t)U.node_size, lo = (uint32_t)U.s0, hi = (uint32_t)U.s1 - 1;
+                int start = U.node_start;
+                for (int d = 0; d < l; ++d) {
+                    const uint32_t sh = size >> 1, st = size - sh;
+                    const bool tail = (lane >> (l - 1 - d)) & 1;
+                    const uint32_t cs = tail ? st : sh;
+                    const float k = merge_coef(cs, size);
+                    lo = merge_index(k, lo);
+                    hi = merge_index(k, hi);
+                    if (tail) start += (int)sh;
+                    size = cs;
+                }
+                R.size = (int)size;
+                R.lo = (int)lo;
+                R.hi = (int)hi;
+                R.start = start;
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            int first = 0, count = 1;
-            for (int l = 0; l < L; ++l) {
-                const int nfirst = first + count;
-                Range r, h, t;
-                int nchild = 0, c0 = 0, c1 = 0;
-                if (lane < count) {
-                    r = ranges[first + lane];
-                    if (r.size <= 1) {          // a leaf is carried unchanged
-                        nchild = 1;
-                        h = r;
-                        c0 = r.hi - r.lo + 1;
-                    } else {
-                        nchild = 2;
-                        const int sh = r.size >> 1, st = r.size - sh;
-                        const float kh = merge_coef((uint32_t)sh, (uint32_t)r.size);
-                        const float kt = merge_coef((uint32_t)st, (uint32_t)r.size);
-                        h.size = sh;
-                        h.lo = (int)merge_index(kh, (uint32_t)r.lo);
-                        h.hi = (int)merge_index(kh, (uint32_t)r.hi);
-                        h.start = r.start;
-                        t.size = st;
-                        t.lo = (int)merge_index(kt, (uint32_t)r.lo);
-                        t.hi = (int)merge_index(kt, (uint32_t)r.hi);
-                        t.start = r.start + sh;
-                        c0 = h.hi - h.lo + 1;
-                        c1 = t.hi - t.lo + 1;
-                    }
-                }
-                const int pos_incl = wave_incl_scan_int(nchild, lane);
-                const int rows_incl = wave_incl_scan_int(c0 + c1, lane);
-                const int total = __shfl(pos_incl, 63, 64);
-                const int total_rows = __shfl(rows_incl, 63, 64);
-                if (lane < count) {
-                    const int pos = nfirst + pos_incl - nchild;
-                    const int rbase = rows_incl - (c0 + c1);
-                    h.base = rbase;
-                    h.child = 0;
-                    ranges[pos] = h;
-                    if (nchild == 2) {
-                        t.base = rbase + c0;
-                        t.child = 0;
-                        ranges[pos + 1] = t;
-                    }
-                    ranges[first + lane].child = pos;
-                }
-                if (lane == 0) {
-                    lv_first[l + 1] = nfirst;
-                    lv_count[l + 1] = total;
-                    lv_rows[l + 1] = total_rows;
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                first = nfirst;
-                count = total;
+            const int c = R.hi - R.lo + 1;
+            const int incl = wave_incl_scan_int(lane < nr ? c : 0, lane);
+            if (lane < nr) {
+                R.base = incl - c;
+                M.ranges[nr - 1 + lane] = R;
             }
+            if (lane == 63) M.nrows[l] = incl;
         }
-        __syncthreads();
-        nrows = lv_rows[L];
-        if (nrows > kMaxRows || nrows * p4 > zrow) {
-            if (tid == 0 && a.error_flag) atomicOr(a.error_flag, 1);
-            return;
+        lds_barrier();
+        const int nb = uni(M.nrows[L]);
+        const Range* lv = &M.ranges[(1 << L) - 1];
+        for (int r = tid; r < nb; r += kConeBlock) {
+            int lo = 0, hi = (1 << L) - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (lv[mid].base <= r) lo = mid; else hi = mid - 1;
+            }
+            const Range R = lv[lo];
+            src_row[r] = R.start + R.lo + (r - R.base);
         }
-        // ---- bottom level: source row of every LDS row, then the load
-        const int bf = lv_first[L], bc = lv_count[L];
-        for (int r = tid; r < nrows; r += kConeBlock) {
-            const Range R = ranges[find_range(ranges, bf, bc, r)];
-            desc[r].x = R.start + R.lo + (r - R.base);
-        }
-        __syncthreads();
-    } else {
-        nrows = (int)it.node_size;
-        if (nrows > kMaxRows || nrows * p4 > zrow) {
-            if (tid == 0 && a.error_flag) atomicOr(a.error_flag, 2);
-            return;
-        }
+    } else if (tid <= L) {
+        M.nrows[tid] = U.node_size;
     }
-    RT_STAMP(0);
-    // ---- fill the bottom level with 16-byte loads.  Row r is global row
-    // grow(r), floats [grow*p, grow*p + p) of a 16-byte aligned buffer, covered
-    // by at most nch aligned float4 chunks: chunk c holds elements
-    // e = 4c + j - al (al = grow*p & 3), kept when 0 <= e < p.  Every thread
-    // issues all its loads before the first LDS write.
-    {
-        const int amax = (p & 3) == 0 ? 0 : ((p & 1) == 0 ? 2 : 3);
-        const int nch = (p + amax + 3) >> 2;                 // chunks per row (upper bound)
-        const int totalc = nrows * nch;
-        float4 v[kFillChunks];
-        int lo[kFillChunks], e0[kFillChunks];
-        int r = div_rows(tid, nch, 1.0f / (float)nch);
-        int c = tid - r * nch;
-        asm volatile("" : "+v"(r), "+v"(c));
-        const int dr = kConeBlock / nch, dc = kConeBlock - (kConeBlock / nch) * nch;
+    lds_barrier();
+}
+
+// Raw buffer resource over `bytes` bytes at p (gfx9 dword3: 32-bit data
+// format); out-of-range buffer loads return 0 and stores are dropped.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* p, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(uni_ptr(const_cast<void*>(p)), (short)0, uni((int)bytes), 0x00020000);
+}
+
+// Fill of a unit's bottom level: 16-byte aligned global loads into
+// registers (issued before the descriptor build, so their latency overlaps
+// it), then scattered element-wise into the dense LDS rows.  A whole unit is
+// one contiguous block of rows; a tile unit is read row by row (its rows come
+// from 2^L separate ranges).  Chunk k of a thread holds elements
+// e[k] .. e[k] + 3 of the LDS segment starting at lo[k]; elements outside
+// [0, len) are dropped.
+struct Fill {
+    float4 v[kFillChunks];
+    int lo[kFillChunks], e[kFillChunks];
+    int len;
+};
+
+__device__ __forceinline__ void fill_issue(const ConeArgs& a, const UnitMeta& M, const UnitView& U,
+                                           const int* src_row, int tid, Fill& F)
+{
+    const int p = U.p;
+    const int nb = uni(M.nrows[U.levels]);
+    const float* src;
+    if (U.src == kSelLeaves) src = a.leaves + (uint64_t)U.trial * a.leaves_stride + U.src_off;
+    else src = (U.src == kSelPing ? a.ping : a.pong) + (uint64_t)U.trial * a.buf_stride + U.buf_off;
+    // transform blocks start 16-byte aligned and are padded to 4 floats
+    const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(src, (((uint32_t)U.m * (uint32_t)p + 3u) & ~3u) * 4u);
+    if (U.mode != kModeTile) {
+        const uint32_t g0 = (uint32_t)U.node_start * (uint32_t)p;
+        const int al = (int)(g0 & 3u);
+        const int n = nb * p;
+        const int nchunks = (n + al + 3) >> 2;
+        F.len = n;
 #pragma unroll
         for (int k = 0; k < kFillChunks; ++k) {
-            const int rr = min(r, nrows - 1);
-            const int grow = tile ? desc[rr].x : (int)it.node_start + rr;
-            const uint64_t g = (uint64_t)grow * p;
-            const int al = (int)(g & 3);
-            int e = 4 * c - al;
-            if (k * kConeBlock + tid >= totalc) e = p;       // inactive chunk
-            if (e < p) v[k] = *reinterpret_cast<const float4*>(src + (g - al) + 4 * c);
-            lo[k] = rr * p4;
-            e0[k] = e;
+            const int c = tid + k * kConeBlock;
+            F.lo[k] = 0;
+            F.e[k] = c < nchunks ? 4 * c - al : n;
+            if (c < nchunks) {
+                const uint32_t off = (g0 - (uint32_t)al + 4u * (uint32_t)c) * 4u;
+                const auto q = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
+                F.v[k] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]),
+                                     __uint_as_float(q[3]));
+            }
+        }
+    } else {
+        const int amax = (p & 3) == 0 ? 0 : ((p & 1) == 0 ? 2 : 3);
+        const int nch = (p + amax + 3) >> 2;                 // chunks per row (upper bound)
+        const int totalc = nb * nch;
+        F.len = p;
+        int r = tid / nch;
+        int c = tid - r * nch;
+        const int dr = kConeBlock / nch, dc = kConeBlock - dr * nch;
+#pragma unroll
+        for (int k = 0; k < kFillChunks; ++k) {
+            const bool on = k * kConeBlock + tid < totalc;
+            const int rr = min(r, nb - 1);
+            const uint32_t g = (uint32_t)src_row[rr] * (uint32_t)p;
+            const int al = (int)(g & 3u);
+            const int e = 4 * c - al;
+            F.lo[k] = rr * p;
+            F.e[k] = on ? e : p;
+            if (on && e < p) {
+                const uint32_t off = (g - (uint32_t)al + 4u * (uint32_t)c) * 4u;
+                const auto q = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
+                F.v[k] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]),
+                                     __uint_as_float(q[3]));
+            }
             r += dr;
             c += dc;
             if (c >= nch) {
@@ -317,207 +355,214 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
                 ++r;
             }
         }
-#pragma unroll
-        for (int k = 0; k < kFillChunks; ++k) {
-            const int e = e0[k];
-            float* row = data + lo[k];
-            if ((unsigned)e < (unsigned)p) row[e] = v[k].x;
-            if ((unsigned)(e + 1) < (unsigned)p) row[e + 1] = v[k].y;
-            if ((unsigned)(e + 2) < (unsigned)p) row[e + 2] = v[k].z;
-            if ((unsigned)(e + 3) < (unsigned)p) row[e + 3] = v[k].w;
-        }
     }
-    __syncthreads();
-    RT_STAMP(1);
+}
 
-    // ---- merge levels, deepest first.  Two barriers per level: the row
-    // descriptors of level l-1 are built while level l is written back.
-    // Descriptor of output row r of level l: (head row | tail row << 16) in
-    // floats, and the roll shift (transforms.hpp:13-27).
-    auto build_desc = [&](int l) {
-        const int orows = tile ? lv_rows[l] : (int)it.node_size;
-        for (int r = tid; r < orows; r += kConeBlock) {
-            int hrow, trow = -1, shift = 0;
-            if (tile) {
-                const Range R = ranges[find_range(ranges, lv_first[l], lv_count[l], r)];
-                const int u = R.lo + (r - R.base);
-                const Range H = ranges[R.child];
-                if (R.size <= 1) {
-                    hrow = H.base + (u - H.lo);
-                } else {
-                    const Range T = ranges[R.child + 1];
-                    const int sh = R.size >> 1, st = R.size - sh;
-                    const int h = (int)merge_index(merge_coef((uint32_t)sh, (uint32_t)R.size), (uint32_t)u);
-                    const int t = (int)merge_index(merge_coef((uint32_t)st, (uint32_t)R.size), (uint32_t)u);
-                    hrow = H.base + (h - H.lo);
-                    trow = T.base + (t - T.lo);
-                    shift = (u - t) % p;
-                }
-            } else {
-                int a0 = 0, sz = (int)it.node_size;
-                for (int d = 0; d < l; ++d) {
-                    if (sz > 1) {
-                        const int hs = sz >> 1;
-                        if (r - a0 < hs) sz = hs;
-                        else { a0 += hs; sz -= hs; }
-                    }
-                }
-                if (sz <= 1) {
-                    hrow = r;
-                } else {
-                    const int s = r - a0;
-                    const int sh = sz >> 1, st = sz - sh;
-                    const int h = (int)merge_index(merge_coef((uint32_t)sh, (uint32_t)sz), (uint32_t)s);
-                    const int t = (int)merge_index(merge_coef((uint32_t)st, (uint32_t)sz), (uint32_t)s);
-                    hrow = a0 + h;
-                    trow = a0 + sh + t;
-                    shift = (s - t) % p;
+__device__ __forceinline__ void fill_land(const Fill& F, float* data)
+{
+    const unsigned len = (unsigned)F.len;
+#pragma unroll
+    for (int k = 0; k < kFillChunks; ++k) {
+        const int e = F.e[k];
+        float* row = data + F.lo[k];
+        if ((unsigned)e < len) row[e] = F.v[k].x;
+        if ((unsigned)(e + 1) < len) row[e + 1] = F.v[k].y;
+        if ((unsigned)(e + 2) < len) row[e + 2] = F.v[k].z;
+        if ((unsigned)(e + 3) < len) row[e + 3] = F.v[k].w;
+    }
+}
+
+// Row descriptor (LDS float offsets of the head and tail rows, roll shift) of
+// output row r at level l; to = -1 for a carried leaf (size-1 node).
+__device__ __forceinline__ void row_desc(const UnitMeta& M, bool tile, int node_size, int l, int r, int p, int& ho,
+                                         int& to, int& sh)
+{
+    if (tile) {
+        const Range* lv = &M.ranges[(1 << l) - 1];
+        int lo = 0, hi = (1 << l) - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (lv[mid].base <= r) lo = mid; else hi = mid - 1;
+        }
+        const Range R = lv[lo];
+        const int u = R.lo + (r - R.base);
+        const Range H = M.ranges[(2 << l) - 1 + 2 * lo];
+        const Range T = M.ranges[(2 << l) + 2 * lo];
+        const uint32_t hs = (uint32_t)R.size >> 1, ts = (uint32_t)R.size - hs;
+        const int h = (int)merge_index(merge_coef(hs, (uint32_t)R.size), (uint32_t)u);
+        const int t = (int)merge_index(merge_coef(ts, (uint32_t)R.size), (uint32_t)u);
+        ho = (H.base + h - H.lo) * p;
+        to = (T.base + t - T.lo) * p;
+        sh = (u - t) % p;
+    } else {
+        int a0 = 0, sz = node_size;
+        for (int d = 0; d < l; ++d) {
+            if (sz > 1) {
+                const int hs = sz >> 1;
+                if (r - a0 < hs) sz = hs;
+                else {
+                    a0 += hs;
+                    sz -= hs;
                 }
             }
-            const int ho = hrow * p4;
-            const int to = trow < 0 ? zrow : trow * p4;
-            desc[r] = make_int2(ho | (to << 16), shift);
         }
-    };
-    for (int i = tid; i < p4; i += kConeBlock) data[zrow + i] = -0.0f;
-    if (L > 0) build_desc(L - 1);
-    __syncthreads();
-    RT_STAMP(2);
+        if (sz <= 1) {
+            ho = r * p;
+            to = -1;
+            sh = 0;
+        } else {
+            const int s = r - a0;
+            const uint32_t hs = (uint32_t)sz >> 1, ts = (uint32_t)sz - hs;
+            const int h = (int)merge_index(merge_coef(hs, (uint32_t)sz), (uint32_t)s);
+            const int t = (int)merge_index(merge_coef(ts, (uint32_t)sz), (uint32_t)s);
+            ho = (a0 + h) * p;
+            to = (a0 + (int)hs + t) * p;
+            sh = (s - t) % p;
+        }
+    }
+}
+
+// Packed row descriptor: head row | tail row << 10 | shift << 20 (tail row
+// kCarried: a size-1 node carried unchanged).  Rows < 1023, shift < 4096.
+constexpr uint32_t kCarried = 1023;
+
+__device__ __forceinline__ uint32_t pack_desc(int ho, int to, int sh, int p)
+{
+    const uint32_t h = (uint32_t)(ho / p), t = to < 0 ? kCarried : (uint32_t)(to / p);
+    return h | (t << 10) | ((uint32_t)sh << 20);
+}
+
+// First table entry of level l: levels 0..l-1 precede it.
+__device__ __forceinline__ int desc_offset(const UnitMeta& M, int l)
+{
+    int o = 0;
+    for (int j = 0; j < l; ++j) o += uni(M.nrows[j]);
+    return o;
+}
+
+// Descriptors of every output row of levels 0..L-1 (thread per entry).
+__device__ __forceinline__ void build_desc_table(const UnitMeta& M, uint32_t* desc, int entries, int p, int L,
+                                                 bool tile, int node_size, int tid)
+{
+    for (int idx = tid; idx < entries; idx += kConeBlock) {
+        int l = 0, r = idx;
+        while (r >= uni(M.nrows[l])) {
+            r -= uni(M.nrows[l]);
+            ++l;
+        }
+        int ho, to, sh;
+        row_desc(M, tile, node_size, l, r, p, ho, to, sh);
+        desc[idx] = pack_desc(ho, to, sh, p);
+    }
+}
+
+// Outputs of level l (rows wave + 8i, bins lane + 64k) into v.
+template <int SMAX, int RW>
+__device__ __forceinline__ void merge_level(const UnitMeta& M, const float* data, const uint32_t* desc,
+                                            bool use_table, int p, int l, bool tile, int node_size, int lane,
+                                            int wave, int nr, float (&v)[RW][SMAX])
+{
+    const int S = (p + 63) >> 6;
+    int ho = 0, to = -1, sh = 0;
+    if (lane < nr) {
+        const int r = wave + kConeWaves * lane;
+        if (use_table) {
+            const uint32_t d = desc[desc_offset(M, l) + r];
+            const uint32_t t = (d >> 10) & 1023u;
+            ho = (int)(d & 1023u) * p;
+            to = t == kCarried ? -1 : (int)t * p;
+            sh = (int)(d >> 20);
+        } else {
+            row_desc(M, tile, node_size, l, r, p, ho, to, sh);
+        }
+    }
+    // Branch-free over rows and (narrow) slots, so the LDS reads of all the
+    // wave's rows are in flight together: rows i >= nr (descriptor of lane i:
+    // head row 0) and slots past p read in-bounds garbage that is never
+    // written back; a carried leaf (to < 0) reads row 0 as its tail and adds
+    // -0.0 instead (x + (-0.0) == x exactly, as the reference's copy).
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+        const int hb = __builtin_amdgcn_readlane(ho, i);
+        const int tb = __builtin_amdgcn_readlane(to, i);
+        const int s = __builtin_amdgcn_readlane(sh, i);
+        // carried: the tail value becomes -0.0 by bit masking (a select on a
+        // uniform condition would be compiled into a branch per slot)
+        const uint32_t keep = tb < 0 ? 0u : 0xFFFFFFFFu;
+        const uint32_t neg0 = ~keep & 0x80000000u;
+        const float* hrow = data + hb + lane;
+        const float* trow = data + (tb < 0 ? 0 : tb);
+#pragma unroll
+        for (int k = 0; k < SMAX; ++k) {
+            if (SMAX <= 5 || k < S) {
+                // bin j = lane + 64k reads T[(j + s) mod p]; j + s < 2p
+                const uint32_t c = (uint32_t)(lane + s + 64 * k);
+                const uint32_t cw = min(c, c - (uint32_t)p);
+                const float t = __uint_as_float((__float_as_uint(trow[cw]) & keep) | neg0);
+                v[i][k] = __fadd_rn(hrow[64 * k], t);
+            }
+        }
+    }
+}
+
+// All merge levels of one unit.  SMAX >= ceil(p/64) slots per row, RW rows per
+// wave (lds_row_capacity(p, SMAX) guarantees ceil(rows/8) <= RW at every level).  With
+// `st` set (a non-final pass), the output level goes from the staging
+// registers straight to global memory at byte offset st_o0 (rows of the tile
+// are one contiguous segment) instead of back into LDS.
+template <int SMAX, int RW>
+__device__ __forceinline__ void merge_levels(const UnitMeta& M, float* data, const uint32_t* desc, bool use_table,
+                                             int p, int L, bool tile, int node_size, int tid, bool st,
+                                             __amdgpu_buffer_rsrc_t rs, uint32_t st_o0)
+{
+    const int lane = tid & 63, wave = tid >> 6;
+    const int S = (p + 63) >> 6;
     for (int l = L - 1; l >= 0; --l) {
-        const int orows = tile ? lv_rows[l] : (int)it.node_size;
-        // Quads: lane-owned groups of 4 consecutive phase bins of one row (rows
-        // are padded to p4).  H is one aligned ds_read_b128, the rolled T four
-        // ds_read_b32, the result one ds_write_b128; pad columns carry garbage
-        // that only ever flows into pad columns.
-        const int totalq = orows * qpr;
-        float4 v[kQuadsPerThread];
-        int r = div_rows(tid, qpr, 1.0f / (float)qpr);
-        int q = tid - r * qpr;
-        // opaque per level: stops LICM from hoisting all per-quad indices out
-        // of the level loop (which spills the register file)
-        asm volatile("" : "+v"(r), "+v"(q));
-        const int dr = kConeBlock / qpr, dq = kConeBlock - (kConeBlock / qpr) * qpr;
-        const int last_row = orows - 1;
+        const int orows = uni(M.nrows[l]);
+        const int nr = uni(orows > wave ? (orows - wave + kConeWaves - 1) / kConeWaves : 0);
+        float v[RW][SMAX];
+        merge_level<SMAX, RW>(M, data, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
+        if (l == 0 && st) {
 #pragma unroll
-        for (int g = 0; g < kQuadsPerThread; g += kMergeGroup) {
-            if (g * kConeBlock < totalq) {         // uniform: whole group inactive otherwise
+            for (int i = 0; i < RW; ++i) {
+                if (i < nr) {
+                    const uint32_t o = st_o0 + (uint32_t)((wave + kConeWaves * i) * p + lane) * 4u;
 #pragma unroll
-                for (int j = 0; j < kMergeGroup && g + j < kQuadsPerThread; ++j) {
-                    const int2 d = desc[min(r, last_row)];
-                    const int ho = d.x & 0xFFFF;
-                    const int to = (int)((unsigned)d.x >> 16);
-                    const int col = q << 2;
-                    const float4 hv = data4[(ho + col) >> 2];   // ho, col multiples of 4
-                    int c0 = col + d.y;
-                    c0 = c0 >= p ? c0 - p : c0;
-                    int c1 = c0 + 1, c2 = c0 + 2, c3 = c0 + 3;
-                    c1 = c1 >= p ? c1 - p : c1;
-                    c2 = c2 >= p ? c2 - p : c2;
-                    c3 = c3 >= p ? c3 - p : c3;
-                    // carried rows point `to` at the -0.0 row: x + (-0.0) == x exactly
-                    v[g + j] = make_float4(__fadd_rn(hv.x, data[to + c0]), __fadd_rn(hv.y, data[to + c1]),
-                                           __fadd_rn(hv.z, data[to + c2]), __fadd_rn(hv.w, data[to + c3]));
-                    r += dr;
-                    q += dq;
-                    const bool wrap = q >= qpr;
-                    q = wrap ? q - qpr : q;
-                    r = wrap ? r + 1 : r;
+                    for (int k = 0; k < SMAX; ++k)
+                        if (k < S && lane + 64 * k < p)
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs,
+                                                                  (int)(o + 256u * (uint32_t)k), 0, 0);
                 }
             }
+            return;
         }
-        __syncthreads();
+        lds_barrier();
 #pragma unroll
-        for (int g = 0; g < kQuadsPerThread; g += kMergeGroup) {
-            if (g * kConeBlock < totalq) {
+        for (int i = 0; i < RW; ++i) {
+            if (i < nr) {
+                float* orow = data + (wave + kConeWaves * i) * p + lane;
 #pragma unroll
-                for (int j = 0; j < kMergeGroup && g + j < kQuadsPerThread; ++j) {
-                    const int qi = (g + j) * kConeBlock + tid;
-                    if (qi < totalq) data4[qi] = v[g + j];
-                }
+                for (int k = 0; k < SMAX; ++k)
+                    if (k < S && lane + 64 * k < p) orow[64 * k] = v[i][k];
             }
         }
-        if (l > 0) build_desc(l - 1);
-        __syncthreads();
-        RT_STAMP(3);
-        nrows = orows;
+        lds_barrier();
     }
+}
 
-    // ---- output: tile rows [s0, s0 + nrows) of the node, one contiguous
-    // global segment written in aligned float4 chunks (segment-end chunks
-    // element-wise).  Chunk c holds segment elements e = 4c + j - al.
-    if (it.dst != kSelSnr) {
-        const uint64_t g0 = (uint64_t)(it.node_start + it.s0) * p;
-        const int al = (int)(g0 & 3);
-        float* dst = (it.dst == kSelPing ? a.ping : a.pong) + trial * a.buf_stride + X.buf_off + (g0 - al);
-        const int total = nrows * p;
-        const int totalc = (total + al + 3) >> 2;
-        float4 v[kFillChunks];
-        // (row, col) of element e = 4*tid - al, stepped by 4*kConeBlock per chunk
-        int e = 4 * tid - al;
-        int r = e < 0 ? -1 : div_rows(e, p, inv_p);
-        int col = e - r * p;
-        asm volatile("" : "+v"(r), "+v"(col));
-        constexpr int kStep = 4 * kConeBlock;
-        const int dr = kStep / p, dc = kStep - (kStep / p) * p;
-#pragma unroll
-        for (int k = 0; k < kFillChunks; ++k) {
-            if (k * kConeBlock + tid < totalc) {
-                float x[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    int cj = col + j, rj = r;
-                    if (cj >= p) {
-                        cj -= p;
-                        ++rj;
-                    }
-                    if (p < 4) {                 // uniform: several wraps inside a chunk
-                        while (cj >= p) {
-                            cj -= p;
-                            ++rj;
-                        }
-                    }
-                    const int ej = e + j;
-                    x[j] = data[((unsigned)ej < (unsigned)total) ? rj * p4 + cj : 0];
-                }
-                v[k] = make_float4(x[0], x[1], x[2], x[3]);
-            }
-            e += kStep;
-            r += dr;
-            col += dc;
-            if (col >= p) {
-                col -= p;
-                ++r;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < kFillChunks; ++k) {
-            const int ci = k * kConeBlock + tid;
-            if (ci < totalc) {
-                const int eb = 4 * ci - al;
-                if (eb >= 0 && eb + 3 < total) {
-                    *reinterpret_cast<float4*>(dst + 4 * ci) = v[k];
-                } else {
-                    if ((unsigned)eb < (unsigned)total) dst[4 * ci] = v[k].x;
-                    if ((unsigned)(eb + 1) < (unsigned)total) dst[4 * ci + 1] = v[k].y;
-                    if ((unsigned)(eb + 2) < (unsigned)total) dst[4 * ci + 2] = v[k].z;
-                    if ((unsigned)(eb + 3) < (unsigned)total) dst[4 * ci + 3] = v[k].w;
-                }
-            }
-        }
-        RT_STAMP(4);
-#ifdef RT_STAMPS
-        if (tid == 0) atomicAdd(&a.stamps[7], 1ull);
-#endif
-        return;
-    }
-
-    // ---- fused boxcar S/N epilogue (snr.hpp:37-65) on the root's rows s < rows_eval
-    const int nev = (int)min((int64_t)nrows, (int64_t)X.rows_eval - (int64_t)it.s0);
+// Fused boxcar S/N (snr.hpp:37-65) of the output rows s < rows_eval held in LDS
+// (row stride p): G lanes per row (G in 8..64, the smallest with
+// ceil(p/G) <= kSnrChunk), each lane a chunk of c <= kSnrChunk columns held in
+// registers; c is odd so the G chunks of a row hit distinct LDS banks.  fp64
+// prefix: sequential in the chunk + log2(G)-step segmented scan
+// (kernels.hpp:73-86).
+__device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& U, float* data, const int* wl, int nrows,
+                                             int tid)
+{
+    const int lane = tid & 63, wave = tid >> 6;
+    const int p = U.p;
+    const int nev = (int)min((int64_t)nrows, (int64_t)U.rows_eval - (int64_t)U.s0);
     if (nev <= 0) return;
-    // G lanes per row (G in 8..64, the smallest with ceil(p/G) <= kSnrChunk),
-    // each lane a chunk of c <= kSnrChunk columns held in registers; c is odd so
-    // the G chunks of a row hit distinct LDS banks.  fp64 prefix: sequential in
-    // the chunk + log2(G)-step segmented scan (kernels.hpp:73-86).
     int G = 8;
     while (G < 64 && ((((p + G - 1) / G) | 1) > kSnrChunk)) G <<= 1;
     int c = (p + G - 1) / G;
@@ -528,12 +573,12 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
     const int owner = (p - 1) / c;
     const int rows_per_pass = kConeBlock / G;
     const uint32_t nw = a.num_widths;
-    float* snr = a.snr + trial * a.snr_stride + (X.snr_row + it.s0) * (uint64_t)nw;
+    float* snr = a.snr + (uint64_t)U.trial * a.snr_stride + (U.snr_row + (uint64_t)U.s0) * (uint64_t)nw;
     if (c <= kSnrChunk) {
         for (int base = 0; base < nev; base += rows_per_pass) {
             const int r = base + (tid / G);
             const bool active = r < nev;
-            float* row = data + min(r, nev - 1) * p4 + j0;
+            float* row = data + min(r, nev - 1) * p + j0;
             const int last = max(cnt - 1, 0);
             float cp[kSnrChunk];
             // branch-free: every lane issues all kSnrChunk reads (clamped to its
@@ -568,12 +613,12 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
                 for (int i = 0; i < kSnrChunk; ++i)
                     if (i < cnt) row[i] = cp[i];
             }
-            __syncthreads();                      // prefix rows visible to all lanes
-            const float* crow = data + min(r, nev - 1) * p4;
+            lds_barrier();                        // prefix rows visible to all lanes
+            const float* crow = data + min(r, nev - 1) * p;
             for (uint32_t iw = 0; iw < nw; ++iw) {
-                const int w = wl[iw];
+                const int w = uni(wl[iw]);
                 float dmax = -INFINITY;
-                constexpr int kB = 11;                    // reads in flight per batch
+                constexpr int kB = 17;                    // reads in flight per batch
                 static_assert(kSnrChunk % kB == 0, "batching");
 #pragma unroll
                 for (int b0 = 0; b0 < kSnrChunk; b0 += kB) {
@@ -599,16 +644,16 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
                 if (active && g == 0) {
                     const float h = sqrtf((float)(p - w) / (float)(p * w));
                     const float b = (float)w / (float)(p - w) * h;
-                    snr[(uint64_t)r * nw + iw] = ((h + b) * dmax - b * sum) / X.stdnoise;
+                    snr[(uint64_t)r * nw + iw] = ((h + b) * dmax - b * sum) / U.stdnoise;
                 }
             }
         }
     } else {
         // very wide rows (p > 64 * kSnrChunk): one wave per row, chunks from LDS
-        for (int base = 0; base < nev; base += kConeBlock / 64) {
+        for (int base = 0; base < nev; base += kConeWaves) {
             const int r = base + wave;
             const bool active = r < nev;
-            float* row = data + min(r, nev - 1) * p4;
+            float* row = data + min(r, nev - 1) * p;
             double part = 0.0;
             for (int j = j0; j < j0 + cnt; ++j) part += (double)row[j];
             double incl = part;
@@ -618,16 +663,16 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
             }
             double acc = __shfl_up(incl, 1, 64);
             if (g == 0) acc = 0.0;
-            __syncthreads();
+            lds_barrier();
             if (active)
                 for (int j = j0; j < j0 + cnt; ++j) {
                     acc += (double)row[j];
                     row[j] = (float)acc;
                 }
             const float sum = __shfl((float)acc, owner, 64);
-            __syncthreads();
+            lds_barrier();
             for (uint32_t iw = 0; iw < nw; ++iw) {
-                const int w = (int)a.widths[iw];
+                const int w = uni(wl[iw]);
                 float dmax = -INFINITY;
                 for (int i = j0; i < j0 + cnt; ++i) {
                     const int k = i + w;
@@ -638,22 +683,116 @@ __global__ __launch_bounds__(kConeBlock) void cone_kernel(ConeArgs a)
                 if (active && g == 0) {
                     const float h = sqrtf((float)(p - w) / (float)(p * w));
                     const float b = (float)w / (float)(p - w) * h;
-                    snr[(uint64_t)r * nw + iw] = ((h + b) * dmax - b * sum) / X.stdnoise;
+                    snr[(uint64_t)r * nw + iw] = ((h + b) * dmax - b * sum) / U.stdnoise;
                 }
             }
-            __syncthreads();
+            lds_barrier();
         }
     }
-    RT_STAMP(5);
+}
+
+// Diagnostic build only (make stamps, -DRT_STAMPS): thread 0 adds the cycles of
+// each phase to a.stamps[phase] (s_memtime; phases end at barriers).
 #ifdef RT_STAMPS
-    if (tid == 0) atomicAdd(&a.stamps[7], 1ull);
+#define RT_STAMP(i)                                                              \
+    do {                                                                         \
+        if (tid == 0 && a.stamps) {                                              \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();          \
+            atomicAdd(&a.stamps[i], t_ - t_stamp);                               \
+            t_stamp = t_;                                                        \
+        }                                                                        \
+    } while (0)
+#else
+#define RT_STAMP(i) do { } while (0)
+#endif
+
+// One kernel per merge slot width SMAX (units with ceil(p/64) <= SMAX), so each
+// gets its own register allocation.  min 4 waves per SIMD: <= 128 VGPRs, two
+// workgroups per CU.
+template <int SMAX>
+__global__ __launch_bounds__(kConeBlock, 4) void cone_kernel(ConeArgs a)
+{
+#ifdef RT_STAMPS
+    unsigned long long t_stamp = __builtin_amdgcn_s_memtime();
+#endif
+    __shared__ float data[kLdsDataFloats + kLdsPadFloats];
+    __shared__ UnitMeta M;
+    __shared__ uint32_t desc[kDescEntries];
+    __shared__ int src_row[kMaxRows];
+    __shared__ int wl[kMaxWidths];   // boxcar widths: LDS reads never wait on the S/N stores in flight
+
+    const int tid = threadIdx.x;
+    const int u = (int)blockIdx.x;
+    if (u >= (int)(a.num_items * a.batch)) return;
+    if (tid < (int)a.num_widths) wl[tid] = (int)a.widths[tid];   // visible after setup's barriers
+    setup_unit(a, u, M, src_row, tid);
+    RT_STAMP(6);
+    const UnitView U = read_view(M);
+    const int p = U.p;
+    const int L = U.levels;
+    const bool tile = U.mode == kModeTile;
+    bool ok = uni(M.nrows[L]) * p <= kLdsDataFloats;
+    for (int l = 0; l <= L; ++l) ok = ok && uni(M.nrows[l]) <= lds_row_capacity((uint32_t)p, SMAX);
+    if (!ok) {
+        if (tid == 0 && a.error_flag) atomicOr(a.error_flag, 1);
+        return;
+    }
+    Fill F;
+    fill_issue(a, M, U, src_row, tid, F);
+    RT_STAMP(0);
+    // row descriptors of every level while the loads are in flight
+    const int entries = desc_offset(M, L);
+    const bool use_table = entries <= kDescEntries;
+    if (use_table) build_desc_table(M, desc, entries, p, L, tile, U.node_size, tid);
+    RT_STAMP(2);
+    fill_land(F, data);
+    lds_barrier();
+    RT_STAMP(1);
+    // ---- merge levels, deepest first; a non-final pass stores its output
+    // level straight from registers (st), a final pass keeps it in LDS for
+    // the S/N epilogue
+    const bool st = U.dst != kSelSnr;
+    const bool st_regs = st && (a.flags & kConeStoreFromRegs);
+    const float* dst = (U.dst == kSelPing ? a.ping : a.pong) + (uint64_t)U.trial * a.buf_stride + U.buf_off;
+    const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(dst, (((uint32_t)U.m * (uint32_t)p + 3u) & ~3u) * 4u);
+    const uint32_t o0 = (uint32_t)(U.node_start + U.s0) * (uint32_t)p * 4u;
+    if (L > 0)
+        merge_levels<SMAX, merge_rows_per_wave(SMAX)>(M, data, desc, use_table, p, L, tile, U.node_size, tid, st_regs, rs,
+                                                      o0);
+    RT_STAMP(3);
+    const int n0 = uni(M.nrows[0]);
+    if (st) {
+        if (L == 0 || !st_regs) {
+            // ---- store the output level from LDS (a single leaf row, or A/B)
+            const int E = n0 * p;
+            for (int e = tid; e < E; e += kConeBlock)
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(data[e]), rs, (int)(o0 + (uint32_t)e * 4u), 0, 0);
+        }
+        RT_STAMP(4);
+    } else {
+        snr_epilogue(a, U, data, wl, n0, tid);
+        RT_STAMP(5);
+    }
+#ifdef RT_STAMPS
+    if (tid == 0 && a.stamps) atomicAdd(&a.stamps[7], 1ull);
 #endif
 }
 
-hipError_t launch_cone(const ConeArgs& args, uint32_t batch, hipStream_t s)
+hipError_t launch_cone(const ConeArgs& args, uint32_t grid, uint32_t smax, hipStream_t s)
 {
-    if (!args.num_items || !batch) return hipSuccess;
-    hipLaunchKernelGGL(cone_kernel, dim3(args.num_items, batch), dim3(kConeBlock), 0, s, args);
+    if (!args.num_items || !args.batch || !grid) return hipSuccess;
+    const dim3 g(grid), b(kConeBlock);
+    switch (smax) {
+    case 1: hipLaunchKernelGGL(cone_kernel<1>, g, b, 0, s, args); break;
+    case 2: hipLaunchKernelGGL(cone_kernel<2>, g, b, 0, s, args); break;
+    case 3: hipLaunchKernelGGL(cone_kernel<3>, g, b, 0, s, args); break;
+    case 4: hipLaunchKernelGGL(cone_kernel<4>, g, b, 0, s, args); break;
+    case 5: hipLaunchKernelGGL(cone_kernel<5>, g, b, 0, s, args); break;
+    case 8: hipLaunchKernelGGL(cone_kernel<8>, g, b, 0, s, args); break;
+    case 16: hipLaunchKernelGGL(cone_kernel<16>, g, b, 0, s, args); break;
+    case kMaxSlots: hipLaunchKernelGGL(cone_kernel<kMaxSlots>, g, b, 0, s, args); break;
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

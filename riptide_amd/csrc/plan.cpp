@@ -128,22 +128,24 @@ ConeNeed cone_need(uint32_t node_size, uint32_t s0, uint32_t s1, int levels, uin
     struct R { uint32_t size, lo, hi; };
     std::vector<R> cur{{node_size, s0, s1 - 1}}, nxt;
     ConeNeed need;
-    const int stride = lds_row_stride(p);
     auto account = [&](const std::vector<R>& lv) {
-        int rows = 0, floats = 0;
-        for (const R& r : lv) {
-            rows += (int)(r.hi - r.lo + 1);
-            floats += (int)(r.hi - r.lo + 1) * stride;
-        }
+        int rows = 0;
+        for (const R& r : lv) rows += (int)(r.hi - r.lo + 1);
         need.max_rows = std::max(need.max_rows, rows);
-        need.max_floats = std::max(need.max_floats, floats);
+        need.max_floats = std::max(need.max_floats, rows * (int)p);
         need.ranges += (int)lv.size();
     };
     account(cur);
     for (int l = 0; l < levels; ++l) {
         nxt.clear();
         for (const R& r : cur) {
-            if (r.size <= 1) { nxt.push_back(r); continue; }
+            // the device range tree assumes 2^l ranges at level l: every node
+            // that is merged has >= 2 rows
+            if (r.size <= 1) {
+                need.degenerate = true;
+                nxt.push_back(r);
+                continue;
+            }
             const uint32_t sh = r.size >> 1, st = r.size - sh;
             const float kh = merge_coef(sh, r.size), kt = merge_coef(st, r.size);
             nxt.push_back({sh, merge_index(kh, r.lo), merge_index(kh, r.hi)});
@@ -155,19 +157,20 @@ ConeNeed cone_need(uint32_t node_size, uint32_t s0, uint32_t s1, int levels, uin
     return need;
 }
 
-static bool fits(const ConeNeed& n, uint32_t p)
+static bool fits(const ConeNeed& n, uint32_t p, int smax)
 {
-    return n.max_rows <= lds_row_capacity(p) && n.max_floats <= kLdsDataFloats && n.ranges <= kMaxRanges;
+    return !n.degenerate && n.max_rows <= lds_row_capacity(p, smax) && n.max_floats <= kLdsDataFloats &&
+           n.ranges <= kMaxRanges;
 }
 
 // Per-transform schedule: list of passes, each a list of (node, tile, levels).
 struct PassItems { std::vector<ConeItem> items; double read = 0, written = 0; };
 
-static void plan_transform(const FfaXform& X, uint32_t xi, std::vector<PassItems>& passes)
+static void plan_transform(const FfaXform& X, uint32_t xi, int smax, std::vector<PassItems>& passes)
 {
     passes.clear();
     const uint32_t m = X.m, p = X.p;
-    const int C = lds_row_capacity(p);
+    const int C = lds_row_capacity(p, smax);
     if (C < 3) throw std::invalid_argument("phase bins too large for the LDS cone kernel");
     // bottom depth: every node at depth db transforms whole in LDS
     int db = 0;
@@ -217,14 +220,14 @@ static void plan_transform(const FfaXform& X, uint32_t xi, std::vector<PassItems
             while (s0 < n.size) {
                 uint32_t K = std::min<uint32_t>((uint32_t)guess, n.size - s0);
                 ConeNeed need = cone_need(n.size, s0, s0 + K, L, p);
-                while (K > 1 && !fits(need, p)) {
+                while (K > 1 && !fits(need, p, smax)) {
                     K -= std::max<uint32_t>(1, K / 32);
                     need = cone_need(n.size, s0, s0 + K, L, p);
                 }
-                if (!fits(need, p)) throw std::invalid_argument("cone tile does not fit in LDS");
+                if (!fits(need, p, smax)) throw std::invalid_argument("cone tile does not fit in LDS");
                 while (s0 + K < n.size) {
                     ConeNeed nn = cone_need(n.size, s0, s0 + K + 1, L, p);
-                    if (!fits(nn, p)) break;
+                    if (!fits(nn, p, smax)) break;
                     need = nn;
                     ++K;
                 }
@@ -248,11 +251,22 @@ static void plan_transform(const FfaXform& X, uint32_t xi, std::vector<PassItems
     }
 }
 
+// Relative cost of a work item: floats through LDS (bottom rows x p) per merge
+// level, plus the load/store.
+static double item_cost(const ConeItem& it, const FfaXform& X)
+{
+    const double rows = it.mode == kModeTile ? (double)(it.s1 - it.s0) + (double)(2u << it.levels)
+                                             : (double)it.node_size;
+    return rows * (double)X.p * ((double)it.levels + 2.0);
+}
+
 void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uint32_t num_widths,
                      uint64_t scratch_budget, ExecPlan& out)
 {
     out = ExecPlan();
     out.xf = xforms;
+    for (const FfaXform& X : xforms)
+        if (!merge_slots(X.p)) throw std::invalid_argument("phase bins too large for the LDS cone kernel");
     const size_t nx = xforms.size();
     size_t g0 = 0;
     uint32_t group = 0;
@@ -272,36 +286,50 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
         sched.assign(g1 - g0, {});
         uint32_t gpasses = 0;
         for (size_t i = g0; i < g1; ++i) {
-            plan_transform(out.xf[i], (uint32_t)i, sched[i - g0]);
+            plan_transform(out.xf[i], (uint32_t)i, merge_slots(out.xf[i].p), sched[i - g0]);
             gpasses = std::max<uint32_t>(gpasses, (uint32_t)sched[i - g0].size());
         }
         out.max_passes = std::max(out.max_passes, gpasses);
+        // one launch per (pass, kernel variant): a variant runs rows of exactly
+        // its slot width (buckets <= 5), so no lane-slot is wasted
+        std::vector<int> buckets;
+        for (size_t i = g0; i < g1; ++i) buckets.push_back(merge_slots(out.xf[i].p));
+        std::sort(buckets.begin(), buckets.end());
+        buckets.erase(std::unique(buckets.begin(), buckets.end()), buckets.end());
         for (uint32_t k = 0; k < gpasses; ++k) {
-            Launch L;
-            L.first = (uint32_t)out.items.size();
-            L.group = group;
-            L.pass = k;
-            for (size_t i = g0; i < g1; ++i) {
-                auto& sp = sched[i - g0];
-                const uint32_t P = (uint32_t)sp.size();
-                if (k >= P) continue;
-                const FfaXform& X = out.xf[i];
-                const uint8_t src = k == 0 ? kSelLeaves : (((P - k) % 2 == 0) ? kSelPing : kSelPong);
-                const bool last = (k == P - 1);
-                const uint8_t dst = last ? (snr_epilogue ? kSelSnr : kSelPing)
-                                         : (((P - 1 - k) % 2 == 0) ? kSelPing : kSelPong);
-                for (ConeItem it : sp[k].items) {
-                    it.src = src;
-                    it.dst = dst;
-                    out.items.push_back(it);
+            for (const int bucket : buckets) {
+                Launch L;
+                L.smax = (uint32_t)bucket;
+                L.first = (uint32_t)out.items.size();
+                L.group = group;
+                L.pass = k;
+                for (size_t i = g0; i < g1; ++i) {
+                    auto& sp = sched[i - g0];
+                    const uint32_t P = (uint32_t)sp.size();
+                    if (k >= P || merge_slots(out.xf[i].p) != bucket) continue;
+                    const FfaXform& X = out.xf[i];
+                    const uint8_t src = k == 0 ? kSelLeaves : (((P - k) % 2 == 0) ? kSelPing : kSelPong);
+                    const bool last = (k == P - 1);
+                    const uint8_t dst = last ? (snr_epilogue ? kSelSnr : kSelPing)
+                                             : (((P - 1 - k) % 2 == 0) ? kSelPing : kSelPong);
+                    for (ConeItem it : sp[k].items) {
+                        it.src = src;
+                        it.dst = dst;
+                        out.items.push_back(it);
+                    }
+                    const double cells = (double)X.m * X.p;
+                    L.cells += (uint64_t)X.m * X.p;
+                    L.alg_bytes += 4.0 * cells + ((last && snr_epilogue) ? 4.0 * X.rows_eval * num_widths : 4.0 * cells);
+                    L.moved_bytes += sp[k].read + ((last && snr_epilogue) ? 4.0 * X.rows_eval * num_widths : sp[k].written);
                 }
-                const double cells = (double)X.m * X.p;
-                L.cells += (uint64_t)X.m * X.p;
-                L.alg_bytes += 4.0 * cells + ((last && snr_epilogue) ? 4.0 * X.rows_eval * num_widths : 4.0 * cells);
-                L.moved_bytes += sp[k].read + ((last && snr_epilogue) ? 4.0 * X.rows_eval * num_widths : sp[k].written);
+                L.count = (uint32_t)out.items.size() - L.first;
+                // longest first, so the launch tail is made of the cheapest units
+                std::stable_sort(out.items.begin() + L.first, out.items.end(),
+                                 [&](const ConeItem& x, const ConeItem& y) {
+                                     return item_cost(x, out.xf[x.xform]) > item_cost(y, out.xf[y.xform]);
+                                 });
+                if (L.count) out.launches.push_back(L);
             }
-            L.count = (uint32_t)out.items.size() - L.first;
-            if (L.count) out.launches.push_back(L);
         }
         g0 = g1;
         ++group;

@@ -51,6 +51,7 @@ void fill_grid(const PgramPlan& plan, double* periods, uint32_t* foldbins);
 struct Launch {
     uint32_t first = 0, count = 0;   // item range
     uint32_t group = 0, pass = 0;
+    uint32_t smax = 0;               // cone kernel variant: merge_slots() of every transform in the launch
     double alg_bytes = 0;            // 4mp read + (4mp | 4*rows_eval*W) write
     double moved_bytes = 0;          // bytes the items actually read + write (cone overlap incl.)
     uint64_t cells = 0;              // sum m*p of the transforms in this launch
@@ -73,7 +74,7 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
                      uint64_t scratch_budget, ExecPlan& out);
 
 // Dependency-cone footprint of one tile (host mirror of the device range tree).
-struct ConeNeed { int max_rows = 0; int max_floats = 0; int ranges = 0; };
+struct ConeNeed { int max_rows = 0; int max_floats = 0; int ranges = 0; bool degenerate = false; };
 ConeNeed cone_need(uint32_t node_size, uint32_t s0, uint32_t s1, int levels, uint32_t p);
 
 }  // namespace rt

@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""A/B of cone-kernel feature bits (RIPTIDE_AMD_CONE_FLAGS, read per launch
+batch) on the cfg2 workload: ms per trial of the periodogram for each value.
+
+usage (GPU box): python tools/ab_flags.py 3,2,1,0
+"""
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    import torch
+    from riptide_amd import engine
+    n = 1 << 23
+    flags = sys.argv[1].split(",") if len(sys.argv) > 1 else ["3", "0"]
+    B = 8
+    plan = engine.PeriodogramPlan.for_search(n, 256e-6, 0.1, 10.0, 240, 260, ducy_max=0.05)
+    x = torch.randn((B, n), device="cuda", dtype=torch.float32)
+    out = torch.empty((B, plan.length, plan.num_widths), device="cuda", dtype=torch.float32)
+    ws = torch.empty(plan.workspace_bytes(B), dtype=torch.uint8, device="cuda")
+    ref = None
+    for rnd in range(2):
+        for f in flags:
+            os.environ["RIPTIDE_AMD_CONE_FLAGS"] = f
+            plan.run(x, out=out, workspace=ws)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(3):
+                plan.run(x, out=out, workspace=ws)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / (3 * B)
+            same = None
+            if ref is None:
+                ref = out.clone()
+            else:
+                same = bool(torch.equal(ref, out))
+            print(json.dumps({"round": rnd, "flags": f, "ms_per_trial": dt * 1e3, "identical_to_first": same}),
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()
