@@ -196,7 +196,7 @@ void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStrea
 {
     a.stamps = g_stamps;
     a.batch = batch;
-    a.flags = kConeAllFeatures;
+    a.flags = kConeDefaultFeatures;
     if (const char* e = std::getenv("RIPTIDE_AMD_CONE_FLAGS")) a.flags = (uint32_t)std::strtoul(e, nullptr, 0);
     for (size_t li = 0; li < P.ex.launches.size(); ++li) {
         const Launch& L = P.ex.launches[li];

@@ -37,6 +37,7 @@ constexpr int kLdsPadFloats = 128;          // slack read (never used) by the un
 constexpr int kMaxRows = 512;               // rows per level (source-row table, descriptors)
 constexpr int kDescEntries = 1024;          // row-descriptor table (all levels of a unit)
 constexpr int kMaxTileLevels = 6;           // L for tile items
+constexpr int kMaxLevels = 11;              // merge levels of any unit (whole units: ceil(log2(kMaxRows)))
 constexpr int kMaxRanges = (1 << (kMaxTileLevels + 1)) - 1;
 constexpr int kMaxWidths = 32;              // boxcar widths handled by the fused S/N epilogue
 constexpr int kSnrChunk = 17;               // S/N epilogue: columns per lane held in registers
@@ -96,7 +97,7 @@ static_assert(sizeof(FfaXform) == 48, "FfaXform layout");
 
 enum : uint8_t { kModeWhole = 0, kModeTile = 1 };
 // cone kernel feature bits (ConeArgs::flags)
-enum : uint32_t { kConeStoreFromRegs = 1u, kConeAllFeatures = 1u };
+enum : uint32_t { kConeStoreFromRegs = 1u, kConeFuseLevels = 2u, kConeDefaultFeatures = 1u };
 enum : uint8_t { kSelLeaves = 0, kSelPing = 1, kSelPong = 2, kSelSnr = 3 };
 
 // One workgroup of one pass.

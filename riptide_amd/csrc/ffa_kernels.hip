@@ -165,7 +165,8 @@ struct UnitView {
 // (which would also wait for the next unit's DMA) is needed after setup.
 struct UnitMeta {
     UnitView view;
-    int nrows[kMaxTileLevels + 1];   // rows of every level (0 = output level)
+    int nrows[kMaxLevels + 1];       // rows of every level (0 = output level)
+    int doff[kMaxLevels + 1];        // first descriptor-table entry of every level
     Range ranges[kMaxRanges];        // tile units: level l holds 2^l ranges at (1 << l) - 1
 };
 
@@ -260,6 +261,13 @@ __device__ __forceinline__ void setup_unit(const ConeArgs& a, int u, UnitMeta& M
             if (lane == 63) M.nrows[l] = incl;
         }
         lds_barrier();
+        if (tid == 0) {
+            int o = 0;
+            for (int l = 0; l <= L; ++l) {
+                M.doff[l] = o;
+                o += M.nrows[l];
+            }
+        }
         const int nb = uni(M.nrows[L]);
         const Range* lv = &M.ranges[(1 << L) - 1];
         for (int r = tid; r < nb; r += kConeBlock) {
@@ -273,6 +281,7 @@ __device__ __forceinline__ void setup_unit(const ConeArgs& a, int u, UnitMeta& M
         }
     } else if (tid <= L) {
         M.nrows[tid] = U.node_size;
+        M.doff[tid] = tid * U.node_size;
     }
     lds_barrier();
 }
@@ -433,12 +442,7 @@ __device__ __forceinline__ uint32_t pack_desc(int ho, int to, int sh, int p)
 }
 
 // First table entry of level l: levels 0..l-1 precede it.
-__device__ __forceinline__ int desc_offset(const UnitMeta& M, int l)
-{
-    int o = 0;
-    for (int j = 0; j < l; ++j) o += uni(M.nrows[j]);
-    return o;
-}
+__device__ __forceinline__ int desc_offset(const UnitMeta& M, int l) { return uni(M.doff[l]); }
 
 // Descriptors of every output row of levels 0..L-1 (thread per entry).
 __device__ __forceinline__ void build_desc_table(const UnitMeta& M, uint32_t* desc, int entries, int p, int L,
@@ -456,8 +460,9 @@ __device__ __forceinline__ void build_desc_table(const UnitMeta& M, uint32_t* de
     }
 }
 
-// Outputs of level l (rows wave + 8i, bins lane + 64k) into v.
-template <int SMAX, int RW>
+// Outputs of level l (rows wave + 8i, bins lane + 64k) into v.  CARRIED:
+// the level may hold size-1 nodes (whole units near their leaves).
+template <int SMAX, int RW, bool CARRIED>
 __device__ __forceinline__ void merge_level(const UnitMeta& M, const float* data, const uint32_t* desc,
                                             bool use_table, int p, int l, bool tile, int node_size, int lane,
                                             int wave, int nr, float (&v)[RW][SMAX])
@@ -479,49 +484,148 @@ __device__ __forceinline__ void merge_level(const UnitMeta& M, const float* data
     // Branch-free over rows and (narrow) slots, so the LDS reads of all the
     // wave's rows are in flight together: rows i >= nr (descriptor of lane i:
     // head row 0) and slots past p read in-bounds garbage that is never
-    // written back; a carried leaf (to < 0) reads row 0 as its tail and adds
-    // -0.0 instead (x + (-0.0) == x exactly, as the reference's copy).
+    // written back.  The rolled tail read of bin j = lane + 64k is
+    // T[j + s] or, past the wrap point (lane >= p - s - 64k), T[j + s - p]:
+    // two per-row base addresses and a compare/select per slot.  A carried
+    // leaf (to < 0) reads row 0 as its tail and adds -0.0 instead
+    // (x + (-0.0) == x exactly, as the reference's copy).
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
         const int hb = __builtin_amdgcn_readlane(ho, i);
         const int tb = __builtin_amdgcn_readlane(to, i);
         const int s = __builtin_amdgcn_readlane(sh, i);
-        // carried: the tail value becomes -0.0 by bit masking (a select on a
-        // uniform condition would be compiled into a branch per slot)
-        const uint32_t keep = tb < 0 ? 0u : 0xFFFFFFFFu;
-        const uint32_t neg0 = ~keep & 0x80000000u;
         const float* hrow = data + hb + lane;
-        const float* trow = data + (tb < 0 ? 0 : tb);
+        const float* ta = data + (tb < 0 ? 0 : tb) + s + lane;   // T[j + s]
+        const float* tw = ta - p;                                 // T[j + s - p]
+        const int thr = p - s;
+        uint32_t keep = 0xFFFFFFFFu, neg0 = 0u;
+        if (CARRIED) {
+            // a select on this uniform condition would become a branch per slot
+            keep = tb < 0 ? 0u : 0xFFFFFFFFu;
+            neg0 = ~keep & 0x80000000u;
+        }
 #pragma unroll
         for (int k = 0; k < SMAX; ++k) {
             if (SMAX <= 5 || k < S) {
-                // bin j = lane + 64k reads T[(j + s) mod p]; j + s < 2p
-                const uint32_t c = (uint32_t)(lane + s + 64 * k);
-                const uint32_t cw = min(c, c - (uint32_t)p);
-                const float t = __uint_as_float((__float_as_uint(trow[cw]) & keep) | neg0);
+                const float* tp = lane >= thr - 64 * k ? tw : ta;
+                float t = tp[64 * k];
+                if (CARRIED) t = __uint_as_float((__float_as_uint(t) & keep) | neg0);
                 v[i][k] = __fadd_rn(hrow[64 * k], t);
             }
         }
     }
 }
 
-// All merge levels of one unit.  SMAX >= ceil(p/64) slots per row, RW rows per
-// wave (lds_row_capacity(p, SMAX) guarantees ceil(rows/8) <= RW at every level).  With
-// `st` set (a non-final pass), the output level goes from the staging
+// Descriptor (LDS float offsets of head and tail rows, shift; tail -1 when
+// carried) of output row r of level l, from the table or computed.
+__device__ __forceinline__ void level_desc(const UnitMeta& M, const uint32_t* desc, bool use_table, int p, int l,
+                                           int r, bool tile, int node_size, int& ho, int& to, int& sh)
+{
+    if (use_table) {
+        const uint32_t d = desc[desc_offset(M, l) + r];
+        const uint32_t t = (d >> 10) & 1023u;
+        ho = (int)(d & 1023u) * p;
+        to = t == kCarried ? -1 : (int)t * p;
+        sh = (int)(d >> 20);
+    } else {
+        row_desc(M, tile, node_size, l, r, p, ho, to, sh);
+    }
+}
+
+// Two merge levels at once: outputs of level l (rows wave + 8i) from the rows
+// of level l + 2 in LDS, into v.  With H = HH + roll(HT, sh) and
+// T = TH + roll(TT, st) the level l + 1 rows of output row r:
+//     out[j] = (HH[j] + HT[j + sh]) + (TH[j + s1] + TT[j + s1 + st])   (mod p)
+// -- exactly the reference's additions, without writing level l + 1 back to
+// LDS.  A carried (size-1) node contributes -0.0 (x + (-0.0) == x).
+template <int SMAX, int RW>
+__device__ __forceinline__ void merge_level2(const UnitMeta& M, const float* data, const uint32_t* desc,
+                                             bool use_table, int p, int l, bool tile, int node_size, int lane,
+                                             int wave, int nr, float (&v)[RW][SMAX])
+{
+    const int S = (p + 63) >> 6;
+    int hh = 0, ht = 0, th = 0, tt = 0, sh = 0, s1 = 0, s13 = 0, flags = 0;
+    if (lane < nr) {
+        const int r = wave + kConeWaves * lane;
+        int ho, to;
+        level_desc(M, desc, use_table, p, l, r, tile, node_size, ho, to, s1);
+        int a, b, sa;
+        level_desc(M, desc, use_table, p, l + 1, ho / p, tile, node_size, a, b, sa);
+        hh = a;
+        ht = b < 0 ? 0 : b;
+        sh = sa;
+        flags = b < 0 ? 1 : 0;                     // HT carried
+        if (to < 0) {
+            flags |= 2;                            // whole tail carried
+        } else {
+            int c, d, sc;
+            level_desc(M, desc, use_table, p, l + 1, to / p, tile, node_size, c, d, sc);
+            th = c;
+            tt = d < 0 ? 0 : d;
+            s13 = s1 + sc >= p ? s1 + sc - p : s1 + sc;
+            if (d < 0) flags |= 4;                 // TT carried
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+        const int bhh = __builtin_amdgcn_readlane(hh, i);
+        const int bht = __builtin_amdgcn_readlane(ht, i);
+        const int bth = __builtin_amdgcn_readlane(th, i);
+        const int btt = __builtin_amdgcn_readlane(tt, i);
+        const int ssh = __builtin_amdgcn_readlane(sh, i);
+        const int ss1 = __builtin_amdgcn_readlane(s1, i);
+        const int ss13 = __builtin_amdgcn_readlane(s13, i);
+        const int fl = __builtin_amdgcn_readlane(flags, i);
+        const uint32_t k_ht = (fl & 1) ? 0u : 0xFFFFFFFFu;
+        const uint32_t k_th = (fl & 2) ? 0u : 0xFFFFFFFFu;
+        const uint32_t k_tt = (fl & 6) ? 0u : 0xFFFFFFFFu;
+        const float* r_hh = data + bhh + lane;
+        const float* r_ht = data + bht;
+        const float* r_th = data + bth;
+        const float* r_tt = data + btt;
+#pragma unroll
+        for (int k = 0; k < SMAX; ++k) {
+            if (SMAX <= 5 || k < S) {
+                const uint32_t j = (uint32_t)(lane + 64 * k);
+                const uint32_t ca = j + (uint32_t)ssh, cb = j + (uint32_t)ss1, cc = j + (uint32_t)ss13;
+                const float x_hh = r_hh[64 * k];
+                const float x_ht = __uint_as_float((__float_as_uint(r_ht[min(ca, ca - (uint32_t)p)]) & k_ht) |
+                                                   (~k_ht & 0x80000000u));
+                const float x_th = __uint_as_float((__float_as_uint(r_th[min(cb, cb - (uint32_t)p)]) & k_th) |
+                                                   (~k_th & 0x80000000u));
+                const float x_tt = __uint_as_float((__float_as_uint(r_tt[min(cc, cc - (uint32_t)p)]) & k_tt) |
+                                                   (~k_tt & 0x80000000u));
+                v[i][k] = __fadd_rn(__fadd_rn(x_hh, x_ht), __fadd_rn(x_th, x_tt));
+            }
+        }
+    }
+}
+
+// All merge levels of one unit, two at a time where possible (a single level
+// first when L is odd).  SMAX >= ceil(p/64) slots per row, RW rows per wave
+// (lds_row_capacity(p, SMAX) guarantees ceil(rows/8) <= RW at every level).
+// With `st` set (a non-final pass), the output level goes from the staging
 // registers straight to global memory at byte offset st_o0 (rows of the tile
 // are one contiguous segment) instead of back into LDS.
 template <int SMAX, int RW>
 __device__ __forceinline__ void merge_levels(const UnitMeta& M, float* data, const uint32_t* desc, bool use_table,
                                              int p, int L, bool tile, int node_size, int tid, bool st,
-                                             __amdgpu_buffer_rsrc_t rs, uint32_t st_o0)
+                                             __amdgpu_buffer_rsrc_t rs, uint32_t st_o0, bool fuse)
 {
     const int lane = tid & 63, wave = tid >> 6;
     const int S = (p + 63) >> 6;
-    for (int l = L - 1; l >= 0; --l) {
+    int top = L;                  // level held in LDS
+    while (top > 0) {
+        const bool two = fuse && top >= 2 && !((top & 1) && top == L);
+        const int l = two ? top - 2 : top - 1;
         const int orows = uni(M.nrows[l]);
         const int nr = uni(orows > wave ? (orows - wave + kConeWaves - 1) / kConeWaves : 0);
         float v[RW][SMAX];
-        merge_level<SMAX, RW>(M, data, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
+        // size-1 nodes exist at depth l only in whole units with node_size >> l < 2
+        const bool carried = !tile && (node_size >> l) < 2;
+        if (two) merge_level2<SMAX, RW>(M, data, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
+        else if (carried) merge_level<SMAX, RW, true>(M, data, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
+        else merge_level<SMAX, RW, false>(M, data, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
         if (l == 0 && st) {
 #pragma unroll
             for (int i = 0; i < RW; ++i) {
@@ -547,6 +651,7 @@ __device__ __forceinline__ void merge_levels(const UnitMeta& M, float* data, con
             }
         }
         lds_barrier();
+        top = l;
     }
 }
 
@@ -758,7 +863,7 @@ __global__ __launch_bounds__(kConeBlock, 4) void cone_kernel(ConeArgs a)
     const uint32_t o0 = (uint32_t)(U.node_start + U.s0) * (uint32_t)p * 4u;
     if (L > 0)
         merge_levels<SMAX, merge_rows_per_wave(SMAX)>(M, data, desc, use_table, p, L, tile, U.node_size, tid, st_regs, rs,
-                                                      o0);
+                                                      o0, (a.flags & kConeFuseLevels) != 0);
     RT_STAMP(3);
     const int n0 = uni(M.nrows[0]);
     if (st) {
