@@ -44,6 +44,20 @@ def synth_batch(torch, B, n, tsamp, seed, device):
     return x
 
 
+def pmc_traffic():
+    """HBM bytes per trial of the cone kernel from the newest committed PMC
+    summary (profiles/*_pmc_cone.json, written by tools/pmc_to_json.py from
+    rocprofv3 FETCH_SIZE/WRITE_SIZE passes), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_cone.json")))   # r01a < r01b < ...: newest last
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return {"hbm_bytes_per_trial": d["hbm_bytes_per_trial"], "source": os.path.relpath(files[-1], REPO),
+            "commit": d.get("commit")}
+
+
 def cpu_baseline(timeout_s=300):
     cmd = [sys.executable, os.path.join(REPO, "oracle", "cpu_baseline.py"), "--trials", "1"]
     try:
@@ -116,6 +130,7 @@ def main():
     stats = plan.stats()
 
     if rank == 0:
+        pmc = pmc_traffic()
         trials = world * B * args.steps
         achieved = cone["alg_bytes"] / (cone["ms"] * 1e-3) / 1e9 if cone["ms"] > 0 else None
         line = {
@@ -147,7 +162,10 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                "traffic": None,
+                "traffic": (pmc["hbm_bytes_per_trial"] * B / stats["launches"]) if pmc else None,
+                "traffic_per_trial": pmc["hbm_bytes_per_trial"] if pmc else None,
+                "traffic_source": pmc["source"] if pmc else None,
+                "alg_bytes_per_launch": stats["alg_bytes"] * B / stats["launches"],
                 "alg_bytes_per_trial": stats["alg_bytes"],
                 "moved_bytes_per_trial": stats["moved_bytes"],
                 "kernel_ms_per_step": cone["ms"] / args.steps,
