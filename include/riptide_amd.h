@@ -145,6 +145,31 @@ int rt_deredden_normalise_device(const float* d_in, size_t size, size_t batch, s
                                  float* d_out, size_t out_stride, void* d_workspace, size_t workspace_bytes,
                                  void* stream);
 
+/* ------------------------- peak detection (device) ------------------------ */
+/* The data-parallel stages of riptide.peak_detection.find_peaks
+ * (peak_detection.py:37-142) over a batch of device periodograms in the
+ * rt_periodogram_device layout (trial b at d_snrs + b * snr_stride, L x W
+ * row-major).  The host finishes each stage with numpy's own expressions
+ * (percentile lerp, polyfit, cluster1d), so the peaks are identical.
+ *
+ * Order statistics of every (trial, width, segment): segment k covers rows
+ * [k * per_seg, (k + 1) * per_seg) (segment_stats, peak_detection.py:71-82);
+ * d_out[((b * W + iw) * nseg + k) * nranks + r] = the ranks[r]-th smallest S/N
+ * of the segment (NaN if the segment holds a NaN).  per_seg <= 4096. */
+int rt_segment_order_stats_device(const float* d_snrs, size_t batch, size_t snr_stride, size_t length,
+                                  size_t num_widths, size_t nseg, size_t per_seg, const uint32_t* ranks,
+                                  size_t nranks, float* d_out, void* stream);
+/* Threshold selection (peak_detection.py:131-133): row i of (trial b, width
+ * iw) is selected when s > polyval(coeffs[b][iw], logf[i]) and s > smin
+ * (fp64, s = float64 of the S/N).  d_coeffs: batch x W x ncoef doubles,
+ * highest degree first (np.poly1d order); d_logf: L doubles (np.log of the
+ * trial frequencies).  Selected rows are appended, in no particular order, to
+ * d_idx[(b * W + iw) * cap ...] and counted in d_counts[b * W + iw] (zeroed
+ * by the call); a count above cap means the list was truncated. */
+int rt_threshold_select_device(const float* d_snrs, size_t batch, size_t snr_stride, size_t length,
+                               size_t num_widths, const double* d_logf, const double* d_coeffs, size_t ncoef,
+                               double smin, uint32_t* d_counts, uint32_t* d_idx, size_t cap, void* stream);
+
 /* ----------------------------- profiling ---------------------------------- */
 /* When enabled, rt_periodogram_device records HIP events around every cone
  * (FFA pass) launch and accumulates their time and algorithmic bytes

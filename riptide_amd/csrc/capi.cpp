@@ -930,6 +930,45 @@ int rt_deredden_normalise_device(const float* d_in, size_t size, size_t batch, s
     });
 }
 
+int rt_segment_order_stats_device(const float* d_snrs, size_t batch, size_t snr_stride, size_t length,
+                                  size_t num_widths, size_t nseg, size_t per_seg, const uint32_t* ranks,
+                                  size_t nranks, float* d_out, void* stream)
+{
+    return guarded([&] {
+        if (!batch || !num_widths || !nseg) return RT_OK;
+        if (per_seg == 0 || nseg * per_seg > length) throw std::invalid_argument("segments exceed the periodogram");
+        if (per_seg > (size_t)kMaxSegmentPoints)
+            throw std::invalid_argument("segment longer than the device sort (4096 points)");
+        if (!nranks || nranks > (size_t)kMaxSegmentRanks) throw std::invalid_argument("1 to 8 ranks per segment");
+        for (size_t r = 0; r < nranks; ++r)
+            if (ranks[r] >= per_seg) throw std::invalid_argument("rank outside the segment");
+        if (batch > 65535 || num_widths > 65535 || nseg > 0x7FFFFFFFull)
+            throw std::invalid_argument("segment grid too large");
+        ck(launch_segment_order_stats(d_snrs, snr_stride, (uint32_t)batch, (uint32_t)num_widths, (uint32_t)nseg,
+                                      (uint32_t)per_seg, ranks, (uint32_t)nranks, d_out, (hipStream_t)stream),
+           "segment_order_stats");
+        return RT_OK;
+    });
+}
+
+int rt_threshold_select_device(const float* d_snrs, size_t batch, size_t snr_stride, size_t length,
+                               size_t num_widths, const double* d_logf, const double* d_coeffs, size_t ncoef,
+                               double smin, uint32_t* d_counts, uint32_t* d_idx, size_t cap, void* stream)
+{
+    return guarded([&] {
+        if (!batch || !num_widths) return RT_OK;
+        if (!ncoef || ncoef > 64) throw std::invalid_argument("1 to 64 polynomial coefficients");
+        if (length > 0xFFFFFFFFull || cap > 0xFFFFFFFFull || batch > 65535 || num_widths > 65535)
+            throw std::invalid_argument("threshold selection too large");
+        hipStream_t s = (hipStream_t)stream;
+        ck(hipMemsetAsync(d_counts, 0, batch * num_widths * sizeof(uint32_t), s), "hipMemsetAsync");
+        ck(launch_threshold_select(d_snrs, snr_stride, (uint32_t)batch, (uint32_t)length, (uint32_t)num_widths, d_logf,
+                                   d_coeffs, (uint32_t)ncoef, smin, d_counts, d_idx, (uint32_t)cap, s),
+           "threshold_select");
+        return RT_OK;
+    });
+}
+
 int rt_profile_enable(int on)
 {
     g_prof.on = on != 0;

@@ -44,6 +44,16 @@ hipError_t launch_cone(const ConeArgs& args, uint32_t grid, uint32_t smax, hipSt
 hipError_t launch_ffa_level(const float* in, float* out, const uint2* d_nodes, uint32_t num_nodes,
                             uint32_t rows, uint32_t p, hipStream_t s);
 
+// peaks_kernels.hip
+constexpr int kMaxSegmentPoints = 4096;   // rows of one peak-detection segment sorted in LDS
+constexpr int kMaxSegmentRanks = 8;       // order statistics per segment (host ranks array)
+hipError_t launch_segment_order_stats(const float* snrs, uint64_t snr_stride, uint32_t batch, uint32_t W,
+                                      uint32_t nseg, uint32_t per_seg, const uint32_t* ranks, uint32_t nranks,
+                                      float* out, hipStream_t s);
+hipError_t launch_threshold_select(const float* snrs, uint64_t snr_stride, uint32_t batch, uint32_t L, uint32_t W,
+                                   const double* logf, const double* coeffs, uint32_t ncoef, double smin,
+                                   uint32_t* counts, uint32_t* idx, uint32_t cap, hipStream_t s);
+
 // aux_kernels.hip
 hipError_t launch_snr_rows(const float* x, uint64_t rows, uint32_t cols, const uint32_t* d_widths,
                            uint32_t nw, float stdnoise, float* cps_scratch, float* out, hipStream_t s);

@@ -1,0 +1,117 @@
+// Peak detection on the device (riptide/peak_detection.py:37-142), the two
+// data-parallel stages of find_peaks over a batch of periodograms:
+//
+//   segment_order_stats_kernel: for every (trial, width, frequency segment),
+//     the order statistics np.percentile(..., (25, 50, 75)) interpolates
+//     between (peak_detection.py:81-83): the segment's S/N values are sorted
+//     in LDS (bitonic, +inf padded) and the requested ranks written out.  The
+//     host finishes the percentiles with numpy's own lerp expressions, the
+//     control points and np.polyfit (a few thousand points per width).
+//   threshold_select_kernel: the dynamic threshold poly(log f) (np.polyval's
+//     Horner loop, fp64, no contraction) and the selection mask
+//     (s > thr) & (s > smin) (peak_detection.py:131-133), compacted into
+//     index lists per (trial, width).  The host sorts each list (np.where
+//     order) and clusters it (cluster1d), which touches only selected points.
+//
+// Both kernels read the periodogram in the engine's [trial][L][W] layout.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "kernels.hpp"
+
+namespace rt {
+
+constexpr int kPeakBlock = 256;
+
+struct SegRanks {           // ranks of the order statistics, passed by value
+    uint32_t r[kMaxSegmentRanks];
+};
+
+__global__ __launch_bounds__(kPeakBlock) void segment_order_stats_kernel(
+    const float* __restrict__ snrs, uint64_t snr_stride, uint32_t W, uint32_t per_seg, uint32_t n2,
+    SegRanks ranks, uint32_t nranks, float* __restrict__ out)
+{
+    __shared__ float key[kMaxSegmentPoints];
+    __shared__ int has_nan;
+    const uint32_t seg = blockIdx.x, iw = blockIdx.y, trial = blockIdx.z;
+    const uint32_t nseg = gridDim.x;
+    const float* s = snrs + (uint64_t)trial * snr_stride + (uint64_t)seg * per_seg * W + iw;
+    if (threadIdx.x == 0) has_nan = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n2; i += kPeakBlock) {
+        float v = INFINITY;
+        if (i < per_seg) {
+            v = s[(uint64_t)i * W];
+            if (v != v) has_nan = 1;
+        }
+        key[i] = v;
+    }
+    __syncthreads();
+    // bitonic sort, ascending
+    for (uint32_t k = 2; k <= n2; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < n2; i += kPeakBlock) {
+                const uint32_t ixj = i ^ j;
+                if (ixj > i) {
+                    const float a = key[i], b = key[ixj];
+                    const bool up = (i & k) == 0;
+                    if ((a > b) == up) {
+                        key[i] = b;
+                        key[ixj] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    float* o = out + (((uint64_t)trial * W + iw) * nseg + seg) * nranks;
+    if (threadIdx.x < nranks) o[threadIdx.x] = has_nan ? NAN : key[ranks.r[threadIdx.x]];
+}
+
+__global__ __launch_bounds__(kPeakBlock) void threshold_select_kernel(
+    const float* __restrict__ snrs, uint64_t snr_stride, uint32_t L, uint32_t W, const double* __restrict__ logf,
+    const double* __restrict__ coeffs, uint32_t ncoef, double smin, uint32_t* __restrict__ counts,
+    uint32_t* __restrict__ idx, uint32_t cap)
+{
+    const uint32_t i = blockIdx.x * kPeakBlock + threadIdx.x;
+    const uint32_t iw = blockIdx.y, trial = blockIdx.z;
+    if (i >= L) return;
+    const double s = (double)snrs[(uint64_t)trial * snr_stride + (uint64_t)i * W + iw];
+    const double* c = coeffs + ((uint64_t)trial * W + iw) * ncoef;
+    const double x = logf[i];
+    double y = 0.0;                                  // np.polyval: y = y * x + pv
+    for (uint32_t k = 0; k < ncoef; ++k) y = __dadd_rn(__dmul_rn(y, x), c[k]);
+    if (s > y && s > smin) {
+        const uint32_t list = trial * W + iw;
+        const uint32_t pos = atomicAdd(&counts[list], 1u);
+        if (pos < cap) idx[(uint64_t)list * cap + pos] = i;
+    }
+}
+
+hipError_t launch_segment_order_stats(const float* snrs, uint64_t snr_stride, uint32_t batch, uint32_t W,
+                                      uint32_t nseg, uint32_t per_seg, const uint32_t* ranks, uint32_t nranks,
+                                      float* out, hipStream_t s)
+{
+    if (!batch || !W || !nseg) return hipSuccess;
+    if (per_seg > (uint32_t)kMaxSegmentPoints || nranks > (uint32_t)kMaxSegmentRanks) return hipErrorInvalidValue;
+    SegRanks rk{};
+    for (uint32_t i = 0; i < nranks; ++i) rk.r[i] = ranks[i];
+    uint32_t n2 = 1;
+    while (n2 < per_seg) n2 <<= 1;
+    hipLaunchKernelGGL(segment_order_stats_kernel, dim3(nseg, W, batch), dim3(kPeakBlock), 0, s, snrs, snr_stride, W,
+                       per_seg, n2, rk, nranks, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_threshold_select(const float* snrs, uint64_t snr_stride, uint32_t batch, uint32_t L, uint32_t W,
+                                   const double* logf, const double* coeffs, uint32_t ncoef, double smin,
+                                   uint32_t* counts, uint32_t* idx, uint32_t cap, hipStream_t s)
+{
+    if (!batch || !W || !L) return hipSuccess;
+    hipLaunchKernelGGL(threshold_select_kernel, dim3((L + kPeakBlock - 1) / kPeakBlock, W, batch), dim3(kPeakBlock), 0,
+                       s, snrs, snr_stride, L, W, logf, coeffs, ncoef, smin, counts, idx, cap);
+    return hipGetLastError();
+}
+
+}  // namespace rt

@@ -287,3 +287,55 @@ def test_full_config(rt, golden_full, name):
     peaks, _ = rt.find_peaks(pg)
     got = [[p.ip, p.iw] for p in peaks]
     assert got == [[p[0], p[1]] for p in g["peaks"]]     # identical candidate list
+
+
+# ---------------------------------------------------------------- device peak detection
+def _device_vs_host_peaks(rt, plan, snr_dev, tobs, dm=0.0, **kw):
+    from riptide_amd.peaks import PeakFinder
+    finder = PeakFinder(plan, tobs, **kw)
+    dev = finder(snr_dev, dms=[dm] * snr_dev.shape[0])
+    periods, foldbins = plan.grid()
+    snrs = snr_dev.cpu().numpy()
+    for b in range(snrs.shape[0]):
+        pg = rt.Periodogram(plan.widths, periods, foldbins, snrs[b], metadata=rt.Metadata({"tobs": tobs, "dm": dm}))
+        ref_peaks, ref_polycos = rt.find_peaks(pg, **kw)
+        got_peaks, got_polycos = dev[b]
+        assert got_peaks == ref_peaks                      # identical Peak tuples, same order
+        for iw in ref_polycos:
+            assert np.array_equal(np.asarray(got_polycos[iw]), np.asarray(ref_polycos[iw]))
+    return dev
+
+
+def test_device_find_peaks_matches_host(rt):
+    import torch
+    from riptide_amd import engine
+    case = inputs.PGRAM_CASES[1]
+    plan = engine.PeriodogramPlan.for_search(case["n"], case["tsamp"], case["pmin"], case["pmax"],
+                                             case["bmin"], case["bmax"], ducy_max=case["ducy_max"])
+    xs = np.stack([inputs.with_signal(case["n"], case["tsamp"], s, 0.41, 14.0) for s in range(4)])
+    d = engine.deredden_normalise(torch.from_numpy(xs).cuda(), 1001, 101)
+    snr = plan.run(d)
+    tobs = case["n"] * case["tsamp"]
+    dev = _device_vs_host_peaks(rt, plan, snr, tobs)
+    assert any(len(p) for p, _ in dev)
+    # a few threshold settings, including the constant-threshold branch (minseg)
+    _device_vs_host_peaks(rt, plan, snr, tobs, smin=5.0, nstd=4.0)
+    _device_vs_host_peaks(rt, plan, snr, tobs, minseg=10 ** 6)
+
+
+@pytest.mark.parametrize("name", ["cfg1", "cfg2"])
+def test_device_find_peaks_full_config(rt, golden_full, name):
+    import torch
+    from riptide_amd import engine
+    from riptide_amd.peaks import PeakFinder
+    g = golden_full["configs"][name]
+    c = g["case"]
+    raw = inputs.full_input(c)
+    if sha(raw) != g["input_sha"]:
+        pytest.skip("input generator differs on this host (numpy RNG/libm); parity not checkable")
+    plan = engine.PeriodogramPlan.for_search(c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"],
+                                             ducy_max=c["ducy_max"])
+    x = engine.deredden_normalise(torch.from_numpy(raw).cuda(), int(round(4.0 / c["tsamp"])), 101)
+    snr = plan.run(x)
+    peaks, _ = PeakFinder(plan, c["n"] * c["tsamp"])(snr, dms=[0.0])[0]
+    assert [[p.ip, p.iw] for p in peaks] == [[p[0], p[1]] for p in g["peaks"]]   # golden candidate list
