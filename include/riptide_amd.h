@@ -170,6 +170,12 @@ int rt_threshold_select_device(const float* d_snrs, size_t batch, size_t snr_str
                                size_t num_widths, const double* d_logf, const double* d_coeffs, size_t ncoef,
                                double smin, uint32_t* d_counts, uint32_t* d_idx, size_t cap, void* stream);
 
+/* --------------------------- file input (device) --------------------------- */
+/* 8-bit SIGPROC samples (riptide/time_series.py:352-357) to float32 in device
+ * memory: d_raw holds n bytes, int8 when is_signed else uint8; exact as
+ * numpy's astype(np.float32).  d_raw must be 4-byte aligned. */
+int rt_convert_samples_device(const void* d_raw, size_t n, int is_signed, float* d_out, void* stream);
+
 /* ----------------------------- profiling ---------------------------------- */
 /* When enabled, rt_periodogram_device records HIP events around every cone
  * (FFA pass) launch and accumulates their time and algorithmic bytes

@@ -969,6 +969,15 @@ int rt_threshold_select_device(const float* d_snrs, size_t batch, size_t snr_str
     });
 }
 
+int rt_convert_samples_device(const void* d_raw, size_t n, int is_signed, float* d_out, void* stream)
+{
+    return guarded([&] {
+        if (n >= (1ull << 42)) throw std::invalid_argument("too many samples");
+        ck(launch_convert_samples(d_raw, n, is_signed, d_out, (hipStream_t)stream), "convert_samples");
+        return RT_OK;
+    });
+}
+
 int rt_profile_enable(int on)
 {
     g_prof.on = on != 0;

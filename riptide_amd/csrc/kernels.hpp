@@ -54,6 +54,8 @@ hipError_t launch_threshold_select(const float* snrs, uint64_t snr_stride, uint3
                                    const double* logf, const double* coeffs, uint32_t ncoef, double smin,
                                    uint32_t* counts, uint32_t* idx, uint32_t cap, hipStream_t s);
 
+hipError_t launch_convert_samples(const void* raw, uint64_t n, int is_signed, float* out, hipStream_t s);
+
 // aux_kernels.hip
 hipError_t launch_snr_rows(const float* x, uint64_t rows, uint32_t cols, const uint32_t* d_widths,
                            uint32_t nw, float stdnoise, float* cps_scratch, float* out, hipStream_t s);

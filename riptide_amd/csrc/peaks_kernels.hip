@@ -114,4 +114,37 @@ hipError_t launch_threshold_select(const float* snrs, uint64_t snr_stride, uint3
     return hipGetLastError();
 }
 
+// 8-bit SIGPROC samples -> float32 (riptide/time_series.py:352-357: numpy
+// astype(np.float32) of int8 / uint8 values, exact).  4 samples per thread.
+__global__ __launch_bounds__(256) void convert_samples_kernel(const uint8_t* __restrict__ raw, uint64_t n,
+                                                              int is_signed, float* __restrict__ out)
+{
+    const uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (i + 3 < n) {
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(raw + i);
+        float4 v;
+        if (is_signed) {
+            v = make_float4((float)(int8_t)(w & 0xFF), (float)(int8_t)((w >> 8) & 0xFF),
+                            (float)(int8_t)((w >> 16) & 0xFF), (float)(int8_t)(w >> 24));
+        } else {
+            v = make_float4((float)(w & 0xFF), (float)((w >> 8) & 0xFF), (float)((w >> 16) & 0xFF), (float)(w >> 24));
+        }
+        out[i] = v.x;
+        out[i + 1] = v.y;
+        out[i + 2] = v.z;
+        out[i + 3] = v.w;
+    } else {
+        for (uint64_t k = i; k < n; ++k) out[k] = is_signed ? (float)(int8_t)raw[k] : (float)raw[k];
+    }
+}
+
+hipError_t launch_convert_samples(const void* raw, uint64_t n, int is_signed, float* out, hipStream_t s)
+{
+    if (!n) return hipSuccess;
+    const uint64_t blocks = (n + 1023) / 1024;
+    hipLaunchKernelGGL(convert_samples_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, (const uint8_t*)raw, n,
+                       is_signed, out);
+    return hipGetLastError();
+}
+
 }  // namespace rt

@@ -15,8 +15,7 @@ import typing
 
 import numpy as np
 
-from .peak_detection import Peak, find_peaks
-from .periodogram import Periodogram
+from .peak_detection import Peak
 
 log = logging.getLogger("riptide.dispatch")
 
@@ -35,7 +34,10 @@ def shard(n_items, rank, world):
 
 
 class EngineSearcher:
-    """Batched GPU search of trials of one length: the hot path."""
+    """Batched GPU search of trials of one length: the hot path.  For every
+    search range: one compiled periodogram plan per (length, tsamp, range)
+    and device peak detection (riptide_amd.peaks.PeakFinder); only the peaks
+    leave the device."""
 
     def __init__(self, deredden_params, range_confs, device=None, batch=8):
         self.deredden_params = dict(deredden_params)
@@ -43,6 +45,7 @@ class EngineSearcher:
         self.device = device
         self.batch = int(batch)
         self._plans = {}
+        self._finders = {}
 
     def _plan(self, n, tsamp, conf):
         from . import engine
@@ -54,30 +57,43 @@ class EngineSearcher:
                 ducy_max=kw.get("ducy_max", 0.2), wtsp=kw.get("wtsp", 1.5), device=self.device)
         return self._plans[key]
 
+    def _finder(self, plan, tobs, conf):
+        from .peaks import PeakFinder
+        kw = conf.get("find_peaks", {}) or {}
+        key = (id(plan), tobs, tuple(sorted(kw.items())))
+        if key not in self._finders:
+            self._finders[key] = PeakFinder(plan, tobs, **kw)
+        return self._finders[key]
+
+    def search_device(self, raw, tsamp, metadatas):
+        """Peaks of every trial of a device batch raw [B, N] (float32): one
+        list per trial, in range order (WorkerPool.process_fname)."""
+        from . import engine
+        B, n = raw.shape
+        ws = int(round(self.deredden_params["rmed_width"] / tsamp))
+        x = engine.deredden_normalise(raw, ws, self.deredden_params["rmed_minpts"])
+        out = [[] for _ in range(B)]
+        dms = [m.get("dm") for m in metadatas]
+        for conf in self.range_confs:
+            plan = self._plan(n, tsamp, conf)
+            snr = plan.run(x)
+            for b, (peaks, _) in enumerate(self._finder(plan, n * tsamp, conf)(snr, dms=dms)):
+                out[b].extend(peaks)
+        return out
+
     def __call__(self, trials):
         import torch
-        from . import engine
         dev = torch.device("cuda", torch.cuda.current_device() if self.device is None else self.device)
         peaks = []
         groups = {}
         for t in trials:
             groups.setdefault((t.data.size, float(t.tsamp)), []).append(t)
         for (n, tsamp), group in groups.items():
-            ws = int(round(self.deredden_params["rmed_width"] / tsamp))
             for b0 in range(0, len(group), self.batch):
                 chunk = group[b0:b0 + self.batch]
                 raw = torch.from_numpy(np.stack([np.asarray(t.data, np.float32) for t in chunk])).to(dev)
-                x = engine.deredden_normalise(raw, ws, self.deredden_params["rmed_minpts"])
-                for conf in self.range_confs:
-                    plan = self._plan(n, tsamp, conf)
-                    snrs = plan.run(x).cpu().numpy()
-                    periods, foldbins = plan.grid()
-                    for t, s in zip(chunk, snrs):
-                        meta = dict(t.metadata)
-                        meta["tobs"] = n * tsamp
-                        pg = Periodogram(plan.widths, periods, foldbins, s, metadata=meta)
-                        found, _ = find_peaks(pg, **conf.get("find_peaks", {}))
-                        peaks.extend(found)
+                for found in self.search_device(raw, tsamp, [t.metadata for t in chunk]):
+                    peaks.extend(found)
         return peaks
 
 

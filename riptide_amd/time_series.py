@@ -1,8 +1,7 @@
 """TimeSeries container (riptide/time_series.py:16-397).
 
 Dereddening and normalisation run as HIP kernels (rt_deredden_normalise).
-File loaders for SIGPROC/PRESTO and folding are outside this round's hot path
-(SURVEY.md §8(f3), §8(f4)).
+SIGPROC / PRESTO loaders: riptide_amd.reading.
 """
 import copy as _copy
 
@@ -89,6 +88,23 @@ class TimeSeries:
     @classmethod
     def from_numpy_array(cls, array, tsamp, copy=False):
         return cls(array, tsamp, copy=copy)
+
+    @classmethod
+    @timing
+    def from_sigproc(cls, fname, extra_keys={}):
+        """SIGPROC dedispersed time series, 8-bit (signedness from the 'signed'
+        header key) or 32-bit float (time_series.py:320-362)."""
+        from .reading import read_sigproc
+        data, meta, tsamp = read_sigproc(fname, extra_keys=extra_keys)
+        return cls(data, tsamp, metadata=meta)
+
+    @classmethod
+    @timing
+    def from_presto_inf(cls, fname):
+        """PRESTO .inf + .dat pair (time_series.py:283-318)."""
+        from .reading import read_presto
+        data, meta, tsamp = read_presto(fname)
+        return cls(data, tsamp, metadata=meta)
 
     @classmethod
     def from_binary(cls, fname, tsamp, dtype=np.float32):

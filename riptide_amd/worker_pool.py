@@ -1,0 +1,57 @@
+"""GPU replacement of rffa's WorkerPool (riptide/pipeline/worker_pool.py:10-70,
+SURVEY.md §8 f2): same constructor arguments and the same
+`process_fname_list(fnames) -> List[Peak]` contract, so Pipeline.search
+(pipeline.py:177-189) can use it unchanged.
+
+Instead of one CPU process per DM trial, the files of a chunk are grouped by
+(length, sampling time) and searched in device batches: raw samples are
+loaded to the GPU (8-bit data converted there), dereddened and normalised
+once per trial (worker_pool.py:53-58), then every search range runs the FFA
+periodogram (one compiled plan per range and series shape) and device peak
+detection (riptide_amd.peaks).  Peaks come back per file in input order and,
+within a file, in range order -- the order WorkerPool.process_fname_list
+returns them in.
+"""
+import logging
+
+from .dispatch import EngineSearcher
+from .reading import load_device_batch, _raw_samples
+
+log = logging.getLogger("riptide.worker_pool")
+
+
+class GpuWorkerPool:
+    """deredden_params : dict (rmed_width, rmed_minpts)
+    range_confs : list of dicts with 'ffa_search' and 'find_peaks' sections
+    processes : accepted for interface compatibility (the device batch size
+        is `batch`)
+    fmt : 'sigproc' or 'presto'
+    """
+
+    def __init__(self, deredden_params, range_confs, processes=1, fmt="presto", batch=8, device=None):
+        self.deredden_params = dict(deredden_params)
+        self.range_confs = list(range_confs)
+        self.processes = int(processes)
+        self.fmt = fmt
+        self.batch = int(batch)
+        self.searcher = EngineSearcher(self.deredden_params, self.range_confs, device=device, batch=self.batch)
+
+    def process_fname(self, fname):
+        return self.process_fname_list([fname])
+
+    def process_fname_list(self, fnames):
+        fnames = list(fnames)
+        shapes = {}
+        for i, fn in enumerate(fnames):
+            raw, meta, tsamp = _raw_samples(fn, self.fmt)
+            shapes.setdefault((raw.size, float(tsamp)), []).append(i)
+        per_file = [None] * len(fnames)
+        for (n, tsamp), idx in shapes.items():
+            for b0 in range(0, len(idx), self.batch):
+                chunk = idx[b0:b0 + self.batch]
+                x, metas, _ = load_device_batch([fnames[i] for i in chunk], self.fmt, device=self.searcher.device)
+                results = self.searcher.search_device(x, tsamp, metas)
+                for i, peaks in zip(chunk, results):
+                    per_file[i] = peaks
+                    log.debug(f"Done searching DM = {metas[chunk.index(i)].get('dm')}, peaks found: {len(peaks)}")
+        return [p for plist in per_file for p in plist]

@@ -339,3 +339,61 @@ def test_device_find_peaks_full_config(rt, golden_full, name):
     snr = plan.run(x)
     peaks, _ = PeakFinder(plan, c["n"] * c["tsamp"])(snr, dms=[0.0])[0]
     assert [[p.ip, p.iw] for p in peaks] == [[p[0], p[1]] for p in g["peaks"]]   # golden candidate list
+
+
+# ---------------------------------------------------------------- file input + GPU worker pool
+def test_device_sample_conversion_exact(tmp_path):
+    import torch
+    from riptide_amd.reading import load_device_batch, write_sigproc
+    rng = np.random.RandomState(5)
+    hdr = {"tsamp": 1e-3, "nbits": 8, "nchans": 1, "refdm": 1.0, "tstart": 58000.0, "src_raj": 0.0,
+           "src_dej": 0.0}
+    for signed, dtype in ((True, np.int8), (False, np.uint8)):
+        data = [rng.randint(np.iinfo(dtype).min, np.iinfo(dtype).max + 1, size=4099).astype(dtype) for _ in range(3)]
+        fns = []
+        for k, d in enumerate(data):
+            fn = str(tmp_path / f"t{int(signed)}_{k}.tim")
+            write_sigproc(fn, d, dict(hdr, signed=signed))
+            fns.append(fn)
+        x, metas, tsamp = load_device_batch(fns, "sigproc")
+        assert x.dtype == torch.float32 and tsamp == 1e-3
+        for k, d in enumerate(data):
+            assert np.array_equal(x[k].cpu().numpy(), d.astype(np.float32))
+        assert metas[0]["dm"] == 1.0
+
+
+def test_gpu_worker_pool_matches_per_file_search(rt, tmp_path):
+    from riptide_amd.reading import write_sigproc
+    from riptide_amd.worker_pool import GpuWorkerPool
+    n, tsamp = 1 << 16, 256e-6
+    fns = []
+    for k in range(5):
+        x = inputs.with_signal(n, tsamp, 300 + k, 0.37 + 0.02 * k, 18.0 if k % 2 == 0 else 0.0)
+        if k == 3:
+            x = np.clip(np.round(x * 20 + 128), 0, 255).astype(np.uint8)    # an 8-bit file in the mix
+            hdr = {"nbits": 8, "signed": False}
+        else:
+            hdr = {"nbits": 32}
+        fn = str(tmp_path / f"DM{k}.tim")
+        write_sigproc(fn, x, dict(hdr, tsamp=tsamp, nchans=1, refdm=float(k), tstart=58000.0, src_raj=0.0,
+                                  src_dej=0.0))
+        fns.append(fn)
+    dered = {"rmed_width": 1.0, "rmed_minpts": 101}
+    ranges = [{"ffa_search": {"period_min": 0.2, "period_max": 1.0, "bins_min": 100, "bins_max": 110},
+               "find_peaks": {"smin": 6.0}},
+              {"ffa_search": {"period_min": 1.0, "period_max": 2.5, "bins_min": 240, "bins_max": 260},
+               "find_peaks": {"smin": 6.0}}]
+    pool = GpuWorkerPool(dered, ranges, fmt="sigproc", batch=2)
+    got = pool.process_fname_list(fns)
+    # WorkerPool.process_fname, file by file (worker_pool.py:47-70)
+    ref = []
+    for fn in fns:
+        ts = rt.TimeSeries.from_sigproc(fn)
+        ts = ts.deredden(dered["rmed_width"], minpts=dered["rmed_minpts"]).normalise()
+        for conf in ranges:
+            kw = dict(conf["ffa_search"], deredden=False, already_normalised=True)
+            _, pg = rt.ffa_search(ts, **kw)
+            peaks, _ = rt.find_peaks(pg, **conf["find_peaks"])
+            ref.extend(peaks)
+    assert len(ref) > 0
+    assert got == ref
