@@ -71,6 +71,10 @@ size_t rt_downsampled_size(size_t size, double f);
 
 /* python_bindings.cpp:151-165  downsample(data, factor) -> out[rt_downsampled_size(size, factor)] */
 int rt_downsample(const float* x, size_t size, double factor, float* out);
+/* Row-wise downsampling of a rows x size array by the same factor: rows x
+ * downsampled_size(size, f) floats (the batched form folding.py's
+ * downsample_vertical needs; same arithmetic as rt_downsample). */
+int rt_downsample_rows(const float* x, size_t rows, size_t size, double f, float* out);
 
 /* periodogram.hpp:63-109  number of trial periods (validates arguments) */
 int rt_periodogram_length(size_t size, double tsamp, double period_min, double period_max,

@@ -37,6 +37,7 @@ _SIGNATURES = {
     "rt_snr2": (_c_i, [_vp, _c_sz, _c_sz, _vp, _c_sz, _c_f, _vp]),
     "rt_downsampled_size": (_c_sz, [_c_sz, _c_d]),
     "rt_downsample": (_c_i, [_vp, _c_sz, _c_d, _vp]),
+    "rt_downsample_rows": (_c_i, [_vp, _c_sz, _c_sz, _c_d, _vp]),
     "rt_periodogram_length": (_c_i, [_c_sz, _c_d, _c_d, _c_d, _c_sz, _c_sz, _psz]),
     "rt_periodogram": (_c_i, [_vp, _c_sz, _c_d, _vp, _c_sz, _c_d, _c_d, _c_sz, _c_sz, _vp, _vp, _vp]),
     "rt_running_median": (_c_i, [_vp, _c_sz, _c_sz, _vp]),

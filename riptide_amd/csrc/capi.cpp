@@ -667,6 +667,35 @@ int rt_downsample(const float* x, size_t size, double f, float* out)
     });
 }
 
+int rt_downsample_rows(const float* x, size_t rows, size_t size, double f, float* out)
+{
+    return guarded([&] {
+        if (!((f > 1.0) & (f <= (double)size)))
+            throw std::invalid_argument("Downsampling factor must verify: 1 < f <= size");
+        if (!rows) return RT_OK;
+        if (rows > 65535) throw std::invalid_argument("at most 65535 rows per call");
+        const size_t n = downsampled_size(size, f);
+        std::lock_guard<std::mutex> lk(g_mu);
+        Context& c = context();
+        float* dx = dev<float>(c, 0, rows * size);
+        float* dz = dev<float>(c, 1, rows * n);
+        DsRung* dr = dev<DsRung>(c, 2, 1);
+        DsRung r{};
+        r.f = f;
+        r.n = n;
+        r.first_block = 0;
+        ds_configure(r);
+        h2d(dx, x, rows * size * 4, c.stream);
+        h2d(dr, &r, sizeof r, c.stream);
+        ck(launch_downsample_ladder(dx, size, size, dr, 1, (uint32_t)((n + r.per_block - 1) / r.per_block), dz, n,
+                                    (uint32_t)rows, c.stream),
+           "downsample");
+        d2h(out, dz, rows * n * 4, c.stream);
+        sync(c.stream);
+        return RT_OK;
+    });
+}
+
 int rt_periodogram_length(size_t size, double tsamp, double pmin, double pmax, size_t bmin, size_t bmax,
                           size_t* length)
 {

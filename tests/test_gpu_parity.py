@@ -397,3 +397,32 @@ def test_gpu_worker_pool_matches_per_file_search(rt, tmp_path):
             ref.extend(peaks)
     assert len(ref) > 0
     assert got == ref
+
+
+# ---------------------------------------------------------------- candidate folding
+def test_fold_matches_oracle_restatement(rt, oracle):
+    from riptide_amd.folding import downsample_rows, fold
+    np.random.seed(7)
+    ts = rt.TimeSeries.generate(60.0, 1e-3, 0.7317, amplitude=30.0)
+    period, bins = 0.7317, 64
+    factor = period / bins / ts.tsamp
+    # folding.py:65-81 with the oracle's strict downsample
+    d = oracle.downsample(ts.data, factor)
+    m = d.size // bins
+    ref = d[:m * bins].reshape(m, bins).copy()
+    ref *= (m * factor) ** -0.5
+    assert np.array_equal(fold(ts, period, bins), ref)
+    assert np.array_equal(fold(ts, period, bins, subints=1), ref.sum(axis=0))
+    sub = fold(ts, period, bins, subints=16)
+    cols = np.ascontiguousarray(ref.T)
+    exp = np.stack([oracle.downsample(c, m / 16) for c in cols]).T
+    assert sub.shape == exp.shape and np.array_equal(sub, exp)
+    assert np.argmax(fold(ts, period, bins, subints=1)) in range(bins)
+    x = np.random.RandomState(1).normal(size=(5, 1000)).astype(np.float32)
+    assert np.array_equal(downsample_rows(x, 3.7), np.stack([oracle.downsample(r, 3.7) for r in x]))
+    with pytest.raises(ValueError):
+        fold(ts, 1000.0, bins)
+    with pytest.raises(ValueError):
+        fold(ts, period, 10 ** 6)
+    with pytest.raises(ValueError):
+        fold(ts, period, bins, subints=10 ** 6)
