@@ -59,7 +59,7 @@ def pmc_traffic():
 
 
 def cpu_baseline(timeout_s=300):
-    cmd = [sys.executable, os.path.join(REPO, "oracle", "cpu_baseline.py"), "--trials", "1"]
+    cmd = [sys.executable, os.path.join(REPO, "oracle", "cpu_baseline.py"), "--trials", "4"]
     try:
         out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, check=True).stdout
         res = json.loads(out.strip().splitlines()[-1])
