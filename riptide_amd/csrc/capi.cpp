@@ -190,11 +190,11 @@ struct DevicePlan {
 
 // Per-phase cycle counters of the cone kernel (RT_STAMPS diagnostic builds).
 unsigned long long* g_stamps = nullptr;
+uint64_t g_stamp_units = 0;      // unit records written since the last reset
 
 // Run all cone launches of an exec plan.
 void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStream_t s)
 {
-    a.stamps = g_stamps;
     a.batch = batch;
     a.flags = kConeDefaultFeatures;
     if (const char* e = std::getenv("RIPTIDE_AMD_CONE_FLAGS")) a.flags = (uint32_t)std::strtoul(e, nullptr, 0);
@@ -205,6 +205,12 @@ void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStrea
         const uint64_t units = (uint64_t)L.count * batch;   // one workgroup per (item, trial)
         if (units > 0x7FFFFFFFull) throw std::invalid_argument("too many cone work units in one launch");
         const uint32_t grid = (uint32_t)units;
+        // diagnostic builds: this launch's unit records follow the previous ones
+        a.stamps = nullptr;
+        if (g_stamps && g_stamp_units + units <= kTimelineCap) {
+            a.stamps = g_stamps + g_stamp_units * kStampRecWords;
+            g_stamp_units += units;
+        }
         ProfRec r{};
         if (g_prof.on) {
             r.a = g_prof.ev();
@@ -1052,12 +1058,27 @@ int rt_diag_stamps(uint64_t* out8, int reset)
 {
     return guarded([&] {
         if (!g_stamps) {
-            ck(hipMalloc(&g_stamps, 8 * sizeof(unsigned long long)), "hipMalloc");
-            ck(hipMemset(g_stamps, 0, 8 * sizeof(unsigned long long)), "hipMemset");
+            ck(hipMalloc(&g_stamps, kTimelineCap * kStampRecWords * sizeof(unsigned long long)), "hipMalloc");
+            ck(hipMemset(g_stamps, 0, kTimelineCap * kStampRecWords * sizeof(unsigned long long)), "hipMemset");
         }
         ck(hipDeviceSynchronize(), "hipDeviceSynchronize");
-        ck(hipMemcpy(out8, g_stamps, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost), "hipMemcpy");
-        if (reset) ck(hipMemset(g_stamps, 0, 8 * sizeof(unsigned long long)), "hipMemset");
+        for (int i = 0; i < 8; ++i) out8[i] = 0;
+        out8[0] = g_stamp_units;
+        if (reset) g_stamp_units = 0;
+        return RT_OK;
+    });
+}
+
+int rt_diag_timeline(uint64_t* out, uint64_t cap, uint64_t* count)
+{
+    return guarded([&] {
+        *count = 0;
+        if (!g_stamps) return RT_OK;
+        ck(hipDeviceSynchronize(), "hipDeviceSynchronize");
+        const uint64_t n = std::min<uint64_t>(std::min<uint64_t>(g_stamp_units, kTimelineCap), cap);
+        *count = n;
+        if (n)
+            ck(hipMemcpy(out, g_stamps, n * kStampRecWords * sizeof(uint64_t), hipMemcpyDeviceToHost), "hipMemcpy");
         return RT_OK;
     });
 }

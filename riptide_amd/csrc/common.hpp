@@ -96,8 +96,24 @@ struct FfaXform {
 static_assert(sizeof(FfaXform) == 48, "FfaXform layout");
 
 enum : uint8_t { kModeWhole = 0, kModeTile = 1 };
+// RT_STAMPS diagnostic builds: one record per work unit of kStampRecWords
+// words: hw id | xcc << 32, kStampMarks s_memtime marks (start, setup done,
+// fill issued, descriptors built, fill landed, merge done, end), shape bits.
+constexpr int kStampMarks = 11;   // + S/N pass 0: prefix, barrier, window, end
+constexpr int kStampRecWords = kStampMarks + 2;
+constexpr uint64_t kTimelineCap = 1u << 21;
 // cone kernel feature bits (ConeArgs::flags)
-enum : uint32_t { kConeStoreFromRegs = 1u, kConeFuseLevels = 2u, kConeDefaultFeatures = 1u };
+enum : uint32_t {
+    kConeStoreFromRegs = 1u,   // non-final passes store the output level straight from registers
+    kConeFuseLevels = 2u,      // two merge levels per LDS round trip
+    kConeFastMerge = 4u,       // SMAX <= 5 merge with per-row wrap-slot specialisation
+    kConeFillVec = 16u,        // fill lands aligned chunks with ds_write_b128
+    kConeDiagNoSnr = 1u << 30, // diagnostics only (wrong results): skip the S/N epilogue
+    kConeDiagNoMerge = 1u << 29, // diagnostics only (wrong results): skip the merge levels
+    kConeDiagNoWrite = 1u << 28, // diagnostics only (wrong results): skip the level write-back
+    kConeDiagNoBarrier = 1u << 27, // diagnostics only (wrong results): no barriers between merge levels
+    kConeDefaultFeatures = 17u
+};
 enum : uint8_t { kSelLeaves = 0, kSelPing = 1, kSelPong = 2, kSelSnr = 3 };
 
 // One workgroup of one pass.

@@ -304,6 +304,7 @@ struct Fill {
     float4 v[kFillChunks];
     int lo[kFillChunks], e[kFillChunks];
     int len;
+    int al;             // whole units: the level buffer starts at data + al (LDS 16-B phase = global phase)
 };
 
 __device__ __forceinline__ void fill_issue(const ConeArgs& a, const UnitMeta& M, const UnitView& U,
@@ -322,6 +323,7 @@ __device__ __forceinline__ void fill_issue(const ConeArgs& a, const UnitMeta& M,
         const int n = nb * p;
         const int nchunks = (n + al + 3) >> 2;
         F.len = n;
+        F.al = al;
 #pragma unroll
         for (int k = 0; k < kFillChunks; ++k) {
             const int c = tid + k * kConeBlock;
@@ -339,6 +341,7 @@ __device__ __forceinline__ void fill_issue(const ConeArgs& a, const UnitMeta& M,
         const int nch = (p + amax + 3) >> 2;                 // chunks per row (upper bound)
         const int totalc = nb * nch;
         F.len = p;
+        F.al = 0;
         int r = tid / nch;
         int c = tid - r * nch;
         const int dr = kConeBlock / nch, dc = kConeBlock - dr * nch;
@@ -367,19 +370,36 @@ __device__ __forceinline__ void fill_issue(const ConeArgs& a, const UnitMeta& M,
     }
 }
 
-__device__ __forceinline__ void fill_land(const Fill& F, float* data)
+// Lands the staged chunks at base = data + F.al.  A chunk whose LDS address is
+// 16-byte aligned and lies wholly inside its segment is one ds_write_b128
+// (8x8-lane groups over 32 banks: conflict-free); the others (segment ends,
+// tile rows of odd phase) are written element-wise.
+__device__ __forceinline__ void fill_land(const Fill& F, float* base, bool vec_ok)
 {
     const unsigned len = (unsigned)F.len;
+    const int al = F.al;
 #pragma unroll
     for (int k = 0; k < kFillChunks; ++k) {
         const int e = F.e[k];
-        float* row = data + F.lo[k];
-        if ((unsigned)e < len) row[e] = F.v[k].x;
-        if ((unsigned)(e + 1) < len) row[e + 1] = F.v[k].y;
-        if ((unsigned)(e + 2) < len) row[e + 2] = F.v[k].z;
-        if ((unsigned)(e + 3) < len) row[e + 3] = F.v[k].w;
+        float* row = base + F.lo[k];
+        const bool vec = vec_ok && e >= 0 && e + 3 < (int)len && ((F.lo[k] + e + al) & 3) == 0;
+        if (vec) {
+            *reinterpret_cast<float4*>(row + e) = F.v[k];
+        } else {
+            if ((unsigned)e < len) row[e] = F.v[k].x;
+            if ((unsigned)(e + 1) < len) row[e + 1] = F.v[k].y;
+            if ((unsigned)(e + 2) < len) row[e + 2] = F.v[k].z;
+            if ((unsigned)(e + 3) < len) row[e + 3] = F.v[k].w;
+        }
     }
 }
+
+// LDS byte address of an LDS pointer.
+__device__ __forceinline__ uint32_t lds_addr(const float* p)
+{
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
+}
+
 
 // Row descriptor (LDS float offsets of the head and tail rows, roll shift) of
 // output row r at level l; to = -1 for a carried leaf (size-1 node).
@@ -460,6 +480,8 @@ __device__ __forceinline__ void build_desc_table(const UnitMeta& M, uint32_t* de
     }
 }
 
+typedef const __attribute__((address_space(3))) float* lds_cptr;
+
 // Outputs of level l (rows wave + 8i, bins lane + 64k) into v.  CARRIED:
 // the level may hold size-1 nodes (whole units near their leaves).
 template <int SMAX, int RW, bool CARRIED>
@@ -495,8 +517,11 @@ __device__ __forceinline__ void merge_level(const UnitMeta& M, const float* data
         const int tb = __builtin_amdgcn_readlane(to, i);
         const int s = __builtin_amdgcn_readlane(sh, i);
         const float* hrow = data + hb + lane;
-        const float* ta = data + (tb < 0 ? 0 : tb) + s + lane;   // T[j + s]
-        const float* tw = ta - p;                                 // T[j + s - p]
+        // T[j + s] and T[j + s - p]: two opaque LDS addresses, so each slot
+        // is one compare + one select, the slot offset 256k an immediate
+        lds_cptr ta = (lds_cptr)(data + (tb < 0 ? 0 : tb) + s + lane);
+        lds_cptr tw = ta - p;
+        asm("" : "+v"(ta), "+v"(tw));
         const int thr = p - s;
         uint32_t keep = 0xFFFFFFFFu, neg0 = 0u;
         if (CARRIED) {
@@ -507,11 +532,75 @@ __device__ __forceinline__ void merge_level(const UnitMeta& M, const float* data
 #pragma unroll
         for (int k = 0; k < SMAX; ++k) {
             if (SMAX <= 5 || k < S) {
-                const float* tp = lane >= thr - 64 * k ? tw : ta;
+                const lds_cptr tp = lane >= thr - 64 * k ? tw : ta;
                 float t = tp[64 * k];
                 if (CARRIED) t = __uint_as_float((__float_as_uint(t) & keep) | neg0);
                 v[i][k] = __fadd_rn(hrow[64 * k], t);
             }
+        }
+    }
+}
+
+// Level l without size-1 nodes, SMAX <= 5 slots (the hot path).  Per row the
+// descriptor is one v_readlane of the packed word (unpacked in SALU); the
+// head, tail and wrapped-tail rows are three VGPR bases (row base + 4 lane)
+// and the slot offsets 256k immediates.  The tail wraps inside slot
+// kw = (p - s) / 64: slots before it read T[j + s], slots after it
+// T[j + s - p], and only slot kw selects per lane -- a uniform switch on kw
+// picks the straight-line variant.
+template <int SMAX, int KW>
+__device__ __forceinline__ void merge_row_slots(lds_cptr hrow, lds_cptr ta, lds_cptr tw, int lane, int thr,
+                                                float (&v)[SMAX])
+{
+#pragma unroll
+    for (int k = 0; k < SMAX; ++k) {
+        float t;
+        if (k < KW) t = ta[64 * k];
+        else if (k > KW) t = tw[64 * k];
+        else t = (lane >= thr - 64 * k ? tw : ta)[64 * k];
+        v[k] = __fadd_rn(hrow[64 * k], t);
+    }
+}
+
+template <int SMAX, int KW>
+struct MergeRowSwitch {
+    __device__ static __forceinline__ void run(int kw, lds_cptr hrow, lds_cptr ta, lds_cptr tw, int lane, int thr,
+                                               float (&v)[SMAX])
+    {
+        if (kw == KW || KW == SMAX) merge_row_slots<SMAX, KW>(hrow, ta, tw, lane, thr, v);
+        else if constexpr (KW < SMAX) MergeRowSwitch<SMAX, KW + 1>::run(kw, hrow, ta, tw, lane, thr, v);
+    }
+};
+
+template <int SMAX, int RW>
+__device__ __forceinline__ void merge_level_fast(const UnitMeta& M, const float* data, const uint32_t* desc,
+                                                 bool use_table, int p, int l, bool tile, int node_size, int lane,
+                                                 int wave, int nr, float (&v)[RW][SMAX])
+{
+    static_assert(SMAX <= 5, "fast merge: SMAX <= 5");
+    uint32_t d = 0;
+    if (lane < nr) {
+        const int r = wave + kConeWaves * lane;
+        if (use_table) {
+            d = desc[desc_offset(M, l) + r];
+        } else {
+            int ho, to, sh;
+            row_desc(M, tile, node_size, l, r, p, ho, to, sh);
+            d = pack_desc(ho, to, sh, p);
+        }
+    }
+    const lds_cptr lbase = (lds_cptr)data + lane;
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+        if (i < nr) {
+            const uint32_t dw = (uint32_t)__builtin_amdgcn_readlane((int)d, i);
+            const int h = (int)(dw & 1023u), t = (int)((dw >> 10) & 1023u), sft = (int)(dw >> 20);
+            lds_cptr hrow = lbase + h * p;
+            lds_cptr ta = lbase + (t * p + sft);
+            lds_cptr tw = lbase + (t * p + sft - p);
+            asm("" : "+v"(ta), "+v"(tw));
+            const int thr = p - sft;
+            MergeRowSwitch<SMAX, 0>::run(thr >> 6, hrow, ta, tw, lane, thr, v[i]);
         }
     }
 }
@@ -610,7 +699,7 @@ __device__ __forceinline__ void merge_level2(const UnitMeta& M, const float* dat
 template <int SMAX, int RW>
 __device__ __forceinline__ void merge_levels(const UnitMeta& M, float* data, const uint32_t* desc, bool use_table,
                                              int p, int L, bool tile, int node_size, int tid, bool st,
-                                             __amdgpu_buffer_rsrc_t rs, uint32_t st_o0, bool fuse)
+                                             __amdgpu_buffer_rsrc_t rs, uint32_t st_o0, bool fuse, uint32_t diag)
 {
     const int lane = tid & 63, wave = tid >> 6;
     const int S = (p + 63) >> 6;
@@ -625,7 +714,10 @@ __device__ __forceinline__ void merge_levels(const UnitMeta& M, float* data, con
         const bool carried = !tile && (node_size >> l) < 2;
         if (two) merge_level2<SMAX, RW>(M, data, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
         else if (carried) merge_level<SMAX, RW, true>(M, data, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
-        else merge_level<SMAX, RW, false>(M, data, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
+        else if (SMAX <= 5 && (diag & kConeFastMerge)) {
+            if constexpr (SMAX <= 5)
+                merge_level_fast<SMAX, RW>(M, data, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
+        } else merge_level<SMAX, RW, false>(M, data, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
         if (l == 0 && st) {
 #pragma unroll
             for (int i = 0; i < RW; ++i) {
@@ -640,29 +732,245 @@ __device__ __forceinline__ void merge_levels(const UnitMeta& M, float* data, con
             }
             return;
         }
-        lds_barrier();
+        if (!(diag & kConeDiagNoBarrier)) lds_barrier();
+        if (diag & kConeDiagNoWrite) {
+        } else {
 #pragma unroll
-        for (int i = 0; i < RW; ++i) {
-            if (i < nr) {
-                float* orow = data + (wave + kConeWaves * i) * p + lane;
+            for (int i = 0; i < RW; ++i) {
+                if (i < nr) {
+                    float* orow = data + (wave + kConeWaves * i) * p + lane;
 #pragma unroll
-                for (int k = 0; k < SMAX; ++k)
-                    if (k < S && lane + 64 * k < p) orow[64 * k] = v[i][k];
+                    for (int k = 0; k < SMAX; ++k) {
+                        if (64 * (k + 1) <= p) orow[64 * k] = v[i][k];            // full slot: no lane mask
+                        else if (k < S && lane + 64 * k < p) orow[64 * k] = v[i][k];
+                    }
+                }
             }
         }
-        lds_barrier();
+        if (!(diag & kConeDiagNoBarrier)) lds_barrier();
         top = l;
     }
 }
 
 // Fused boxcar S/N (snr.hpp:37-65) of the output rows s < rows_eval held in LDS
-// (row stride p): G lanes per row (G in 8..64, the smallest with
-// ceil(p/G) <= kSnrChunk), each lane a chunk of c <= kSnrChunk columns held in
-// registers; c is odd so the G chunks of a row hit distinct LDS banks.  fp64
-// prefix: sequential in the chunk + log2(G)-step segmented scan
-// (kernels.hpp:73-86).
+// (row stride p): G lanes per row, each lane a chunk of c <= CH columns held
+// in registers (c odd: the G chunks of a row start on distinct banks).
+// fp64 prefix: sequential in the chunk + log2(G)-step segmented scan
+// (kernels.hpp:73-86).  For G <= 16 (one DPP row) the scan, the per-width
+// max and the neighbour exchange run on DPP row shifts (VALU, no LDS
+// round trip); each lane then reads its window c[j0 .. j0 + CH + kSnrWin)
+// (the wrap c[p + j] = c[j] + sum applied once per element) and evaluates
+// every width w <= kSnrWin from registers.  Wider rows and wider widths use
+// the general path (shuffles, LDS reads per width).
+constexpr int kSnrWin = 12;
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v)
+{
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, true);
+    return __hiloint2double(hi, lo);
+}
+
+// row_shr:d within 16-lane rows: lane g (of a G-lane group, G <= 16) takes
+// lane g - d of its group when g >= d.
+template <int G>
+__device__ __forceinline__ double seg_scan_dpp(double v, int g)
+{
+    double y = dpp_d<0x111>(v);
+    v = g >= 1 ? v + y : v;
+    y = dpp_d<0x112>(v);
+    v = g >= 2 ? v + y : v;
+    y = dpp_d<0x114>(v);
+    v = g >= 4 ? v + y : v;
+    if (G == 16) {
+        y = dpp_d<0x118>(v);
+        v = g >= 8 ? v + y : v;
+    }
+    return v;
+}
+
+// row_shr:d keeping the lane's own value where the source is outside the
+// 16-lane row (bound_ctrl off, old = v)
+template <int CTRL>
+__device__ __forceinline__ float dpp_keep(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// max over the G lanes of a group, valid in lane g == G - 1.  fmaxf never
+// returns a NaN operand over a number, as diff_max's comparison.
+template <int G>
+__device__ __forceinline__ float seg_max_dpp(float v, int g)
+{
+    if constexpr (G == 16) {
+        v = fmaxf(v, dpp_keep<0x111>(v));
+        v = fmaxf(v, dpp_keep<0x112>(v));
+        v = fmaxf(v, dpp_keep<0x114>(v));
+        v = fmaxf(v, dpp_keep<0x118>(v));
+    } else {
+        float y = dpp_keep<0x111>(v);
+        v = g >= 1 ? fmaxf(v, y) : v;
+        y = dpp_keep<0x112>(v);
+        v = g >= 2 ? fmaxf(v, y) : v;
+        y = dpp_keep<0x114>(v);
+        v = g >= 4 ? fmaxf(v, y) : v;
+    }
+    return v;
+}
+
+// diff_max (kernels.hpp:50-60) of width W over the lane's columns (cp[i] =
+// +inf past the lane's chunk, so those differences are -inf)
+template <int CH, int W>
+__device__ __forceinline__ float window_max(const float (&z)[CH + kSnrWin], const float (&cp)[CH])
+{
+    float dm = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) dm = fmaxf(dm, __fsub_rn(z[i + W], cp[i]));
+    return dm;
+}
+
+template <int CH, int W>
+struct WindowSwitch {
+    __device__ static __forceinline__ float run(int w, const float (&z)[CH + kSnrWin], const float (&cp)[CH])
+    {
+        if (w == W) return window_max<CH, W>(z, cp);
+        if constexpr (W < kSnrWin) return WindowSwitch<CH, W + 1>::run(w, z, cp);
+        return -INFINITY;
+    }
+};
+
+#ifdef RT_STAMPS
+#define RT_SNR_MARK(i)                                                           \
+    do {                                                                         \
+        if (tid == 0 && base == 0 && tl) tl[i] = __builtin_amdgcn_s_memtime();   \
+    } while (0)
+#else
+#define RT_SNR_MARK(i) do { } while (0)
+#endif
+
+template <int CH, int G>
+__device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, float* data, const int* wl, int nev,
+                                         int c, int tid, unsigned long long* tl)
+{
+    constexpr bool kDpp = G <= 16;
+    const int lane = tid & 63;
+    const int p = U.p;
+    const int g = lane & (G - 1);
+    const int j0 = min(g * c, p);
+    const int cnt = min(j0 + c, p) - j0;          // columns of this lane (may be 0)
+    const int owner = (p - 1) / c;
+    const int rows_per_pass = kConeBlock / G;
+    const int writer = kDpp ? G - 1 : 0;
+    const uint32_t nw = a.num_widths;
+    float* snr = a.snr + (uint64_t)U.trial * a.snr_stride + (U.snr_row + (uint64_t)U.s0) * (uint64_t)nw;
+    for (int base = 0; base < nev; base += rows_per_pass) {
+        const int r = base + (tid / G);
+        const bool active = r < nev;
+        float* row = data + min(r, nev - 1) * p + j0;
+        float cp[CH];
+        // every lane reads CH columns at immediate offsets (past its chunk:
+        // the next chunk, the next row or the LDS pad), masked to 0
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+            const float x = row[i];
+            cp[i] = i < cnt ? x : 0.0f;
+        }
+        // fp64 prefix: the masked columns add +0.0 (the partial sums start at
+        // +0.0 and are never -0.0, so the additions are exact no-ops)
+        double part = 0.0;
+#pragma unroll
+        for (int i = 0; i < CH; ++i) part = part + (double)cp[i];
+        double acc;
+        if constexpr (kDpp) {
+            const double incl = seg_scan_dpp<G>(part, g);
+            acc = dpp_d<0x111>(incl);
+        } else {
+            double incl = part;
+            for (int d = 1; d < G; d <<= 1) {
+                const double y = __shfl_up(incl, d, G);
+                if (g >= d) incl += y;
+            }
+            acc = __shfl_up(incl, 1, G);
+        }
+        if (g == 0) acc = 0.0;
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+            acc = acc + (double)cp[i];
+            cp[i] = (float)acc;
+        }
+        const float sum = __shfl((float)acc, owner, G);
+        if (active) {
+#pragma unroll
+            for (int i = 0; i < CH; ++i)
+                if (i < cnt) row[i] = cp[i];
+        }
+#pragma unroll
+        for (int i = 0; i < CH; ++i) cp[i] = i < cnt ? cp[i] : INFINITY;
+        RT_SNR_MARK(7);
+        lds_barrier();                        // prefix rows visible to all lanes
+        RT_SNR_MARK(8);
+        const float* crow = data + min(r, nev - 1) * p;
+        float z[CH + kSnrWin];                // c[j0 + k], wrap c[p + j] = c[j] + sum applied
+        bool have_z = false;
+        for (uint32_t iw = 0; iw < nw; ++iw) {
+            const int w = uni(wl[iw]);
+            float dmax;
+            if (kDpp && w <= kSnrWin) {
+                if (!have_z) {
+                    // two opaque bases (row and row - p), slot offsets immediate
+                    lds_cptr za = (lds_cptr)(crow + j0);
+                    lds_cptr zb = za - p;
+                    asm("" : "+v"(za), "+v"(zb));
+#pragma unroll
+                    for (int k = 0; k < CH + kSnrWin; ++k) {
+                        const bool wrap = j0 + k >= p;
+                        const float va = za[k], vb = zb[k];
+                        z[k] = wrap ? __fadd_rn(vb, sum) : va;
+                    }
+                    have_z = true;
+                    RT_SNR_MARK(9);
+                }
+                dmax = WindowSwitch<CH, 1>::run(w, z, cp);
+            } else {
+                dmax = -INFINITY;
+                const int last = max(cnt - 1, 0);
+                float lv[CH];
+#pragma unroll
+                for (int t = 0; t < CH; ++t) {
+                    const int k = j0 + min(t, last) + w;
+                    lv[t] = crow[k >= p ? k - p : k];
+                }
+#pragma unroll
+                for (int i = 0; i < CH; ++i) {
+                    const bool wrap = j0 + min(i, last) + w >= p;
+                    const float ck = wrap ? __fadd_rn(lv[i], sum) : lv[i];
+                    dmax = fmaxf(dmax, __fsub_rn(ck, cp[i]));  // diff_max, kernels.hpp:50-60
+                }
+            }
+            if constexpr (kDpp) {
+                dmax = seg_max_dpp<G>(dmax, g);
+            } else {
+                for (int o = G >> 1; o > 0; o >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, o, G));
+            }
+            if (active && g == writer) {
+                const float h = sqrtf((float)(p - w) / (float)(p * w));
+                const float b = (float)w / (float)(p - w) * h;
+                snr[(uint64_t)r * nw + iw] = ((h + b) * dmax - b * sum) / U.stdnoise;
+            }
+        }
+        RT_SNR_MARK(10);
+    }
+}
+
 __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& U, float* data, const int* wl, int nrows,
-                                             int tid)
+                                             int tid, unsigned long long* tl)
 {
     const int lane = tid & 63, wave = tid >> 6;
     const int p = U.p;
@@ -672,89 +980,23 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
     while (G < 64 && ((((p + G - 1) / G) | 1) > kSnrChunk)) G <<= 1;
     int c = (p + G - 1) / G;
     if (c < kSnrChunk) c |= 1;
-    const int g = lane & (G - 1);
-    const int j0 = min(g * c, p);
-    const int cnt = min(j0 + c, p) - j0;          // columns of this lane (may be 0)
-    const int owner = (p - 1) / c;
-    const int rows_per_pass = kConeBlock / G;
     const uint32_t nw = a.num_widths;
     float* snr = a.snr + (uint64_t)U.trial * a.snr_stride + (U.snr_row + (uint64_t)U.s0) * (uint64_t)nw;
-    if (c <= kSnrChunk) {
-        for (int base = 0; base < nev; base += rows_per_pass) {
-            const int r = base + (tid / G);
-            const bool active = r < nev;
-            float* row = data + min(r, nev - 1) * p + j0;
-            const int last = max(cnt - 1, 0);
-            float cp[kSnrChunk];
-            // branch-free: every lane issues all kSnrChunk reads (clamped to its
-            // chunk), values past the chunk are masked
-#pragma unroll
-            for (int i = 0; i < kSnrChunk; ++i) {
-                const float x = row[min(i, last)];
-                cp[i] = i < cnt ? x : 0.0f;
-            }
-            double part = 0.0;
-#pragma unroll
-            for (int i = 0; i < kSnrChunk; ++i) {
-                const double t = part + (double)cp[i];
-                part = i < cnt ? t : part;
-            }
-            double incl = part;
-            for (int d = 1; d < G; d <<= 1) {
-                const double y = __shfl_up(incl, d, G);
-                if (g >= d) incl += y;
-            }
-            double acc = __shfl_up(incl, 1, G);
-            if (g == 0) acc = 0.0;
-#pragma unroll
-            for (int i = 0; i < kSnrChunk; ++i) {
-                const double t = acc + (double)cp[i];
-                acc = i < cnt ? t : acc;
-                cp[i] = (float)acc;
-            }
-            const float sum = __shfl((float)acc, owner, G);
-            if (active) {
-#pragma unroll
-                for (int i = 0; i < kSnrChunk; ++i)
-                    if (i < cnt) row[i] = cp[i];
-            }
-            lds_barrier();                        // prefix rows visible to all lanes
-            const float* crow = data + min(r, nev - 1) * p;
-            for (uint32_t iw = 0; iw < nw; ++iw) {
-                const int w = uni(wl[iw]);
-                float dmax = -INFINITY;
-                constexpr int kB = 17;                    // reads in flight per batch
-                static_assert(kSnrChunk % kB == 0, "batching");
-#pragma unroll
-                for (int b0 = 0; b0 < kSnrChunk; b0 += kB) {
-                    float lv[kB];
-#pragma unroll
-                    for (int t = 0; t < kB; ++t) {
-                        const int k = j0 + min(b0 + t, last) + w;
-                        lv[t] = crow[k >= p ? k - p : k];
-                    }
-#pragma unroll
-                    for (int t = 0; t < kB; ++t) {
-                        const int i = b0 + t;
-                        const bool wrap = j0 + min(i, last) + w >= p;
-                        const float ck = wrap ? __fadd_rn(lv[t], sum) : lv[t];
-                        const float d = __fsub_rn(ck, cp[i]);
-                        dmax = (i < cnt && d > dmax) ? d : dmax;  // diff_max, kernels.hpp:50-60
-                    }
-                }
-                for (int o = G >> 1; o > 0; o >>= 1) {
-                    const float y = __shfl_xor(dmax, o, G);
-                    dmax = y > dmax ? y : dmax;
-                }
-                if (active && g == 0) {
-                    const float h = sqrtf((float)(p - w) / (float)(p * w));
-                    const float b = (float)w / (float)(p - w) * h;
-                    snr[(uint64_t)r * nw + iw] = ((h + b) * dmax - b * sum) / U.stdnoise;
-                }
-            }
-        }
+    if (G == 8) {
+        if (c <= 9) snr_rows<9, 8>(a, U, data, wl, nev, c, tid, tl);
+        else snr_rows<kSnrChunk, 8>(a, U, data, wl, nev, c, tid, tl);
+    } else if (G == 16) {
+        snr_rows<kSnrChunk, 16>(a, U, data, wl, nev, c, tid, tl);
+    } else if (G == 32) {
+        snr_rows<kSnrChunk, 32>(a, U, data, wl, nev, c, tid, tl);
+    } else if (c <= kSnrChunk) {
+        snr_rows<kSnrChunk, 64>(a, U, data, wl, nev, c, tid, tl);
     } else {
         // very wide rows (p > 64 * kSnrChunk): one wave per row, chunks from LDS
+        const int g = lane;
+        const int j0 = min(g * c, p);
+        const int cnt = min(j0 + c, p) - j0;
+        const int owner = (p - 1) / c;
         for (int base = 0; base < nev; base += kConeWaves) {
             const int r = base + wave;
             const bool active = r < nev;
@@ -796,19 +1038,17 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
     }
 }
 
-// Diagnostic build only (make stamps, -DRT_STAMPS): thread 0 adds the cycles of
-// each phase to a.stamps[phase] (s_memtime; phases end at barriers).
+// Diagnostic build only (make stamps, -DRT_STAMPS): thread 0 of every unit
+// writes one record of s_memtime marks at phase boundaries to a.stamps +
+// kStampRecWords * u (the host offsets a.stamps per launch; no atomics, so
+// the timing is not perturbed by contention).
 #ifdef RT_STAMPS
-#define RT_STAMP(i)                                                              \
+#define RT_MARK(i)                                                               \
     do {                                                                         \
-        if (tid == 0 && a.stamps) {                                              \
-            const unsigned long long t_ = __builtin_amdgcn_s_memtime();          \
-            atomicAdd(&a.stamps[i], t_ - t_stamp);                               \
-            t_stamp = t_;                                                        \
-        }                                                                        \
+        if (tid == 0) tl[i] = __builtin_amdgcn_s_memtime();                      \
     } while (0)
 #else
-#define RT_STAMP(i) do { } while (0)
+#define RT_MARK(i) do { } while (0)
 #endif
 
 // One kernel per merge slot width SMAX (units with ceil(p/64) <= SMAX), so each
@@ -818,9 +1058,10 @@ template <int SMAX>
 __global__ __launch_bounds__(kConeBlock, 4) void cone_kernel(ConeArgs a)
 {
 #ifdef RT_STAMPS
-    unsigned long long t_stamp = __builtin_amdgcn_s_memtime();
+    unsigned long long tl[kStampMarks] = {};
+    tl[0] = __builtin_amdgcn_s_memtime();
 #endif
-    __shared__ float data[kLdsDataFloats + kLdsPadFloats];
+    __shared__ __attribute__((aligned(16))) float data[kLdsDataFloats + kLdsPadFloats];
     __shared__ UnitMeta M;
     __shared__ uint32_t desc[kDescEntries];
     __shared__ int src_row[kMaxRows];
@@ -831,7 +1072,7 @@ __global__ __launch_bounds__(kConeBlock, 4) void cone_kernel(ConeArgs a)
     if (u >= (int)(a.num_items * a.batch)) return;
     if (tid < (int)a.num_widths) wl[tid] = (int)a.widths[tid];   // visible after setup's barriers
     setup_unit(a, u, M, src_row, tid);
-    RT_STAMP(6);
+    RT_MARK(1);
     const UnitView U = read_view(M);
     const int p = U.p;
     const int L = U.levels;
@@ -844,15 +1085,16 @@ __global__ __launch_bounds__(kConeBlock, 4) void cone_kernel(ConeArgs a)
     }
     Fill F;
     fill_issue(a, M, U, src_row, tid, F);
-    RT_STAMP(0);
+    RT_MARK(2);
     // row descriptors of every level while the loads are in flight
     const int entries = desc_offset(M, L);
     const bool use_table = entries <= kDescEntries;
     if (use_table) build_desc_table(M, desc, entries, p, L, tile, U.node_size, tid);
-    RT_STAMP(2);
-    fill_land(F, data);
+    RT_MARK(3);
+    float* const base = data + uni(F.al);
+    fill_land(F, base, (a.flags & kConeFillVec) != 0);
     lds_barrier();
-    RT_STAMP(1);
+    RT_MARK(4);
     // ---- merge levels, deepest first; a non-final pass stores its output
     // level straight from registers (st), a final pass keeps it in LDS for
     // the S/N epilogue
@@ -861,25 +1103,41 @@ __global__ __launch_bounds__(kConeBlock, 4) void cone_kernel(ConeArgs a)
     const float* dst = (U.dst == kSelPing ? a.ping : a.pong) + (uint64_t)U.trial * a.buf_stride + U.buf_off;
     const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(dst, (((uint32_t)U.m * (uint32_t)p + 3u) & ~3u) * 4u);
     const uint32_t o0 = (uint32_t)(U.node_start + U.s0) * (uint32_t)p * 4u;
-    if (L > 0)
-        merge_levels<SMAX, merge_rows_per_wave(SMAX)>(M, data, desc, use_table, p, L, tile, U.node_size, tid, st_regs, rs,
-                                                      o0, (a.flags & kConeFuseLevels) != 0);
-    RT_STAMP(3);
+    if (L > 0 && !(a.flags & kConeDiagNoMerge))
+        merge_levels<SMAX, merge_rows_per_wave(SMAX)>(M, base, desc, use_table, p, L, tile, U.node_size, tid, st_regs, rs,
+                                                      o0, (a.flags & kConeFuseLevels) != 0,
+                                                      a.flags);
+    RT_MARK(5);
     const int n0 = uni(M.nrows[0]);
     if (st) {
         if (L == 0 || !st_regs) {
             // ---- store the output level from LDS (a single leaf row, or A/B)
             const int E = n0 * p;
             for (int e = tid; e < E; e += kConeBlock)
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(data[e]), rs, (int)(o0 + (uint32_t)e * 4u), 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(base[e]), rs, (int)(o0 + (uint32_t)e * 4u), 0, 0);
         }
-        RT_STAMP(4);
+
     } else {
-        snr_epilogue(a, U, data, wl, n0, tid);
-        RT_STAMP(5);
+#ifdef RT_STAMPS
+        if (!(a.flags & kConeDiagNoSnr)) snr_epilogue(a, U, base, wl, n0, tid, tl);
+#else
+        if (!(a.flags & kConeDiagNoSnr)) snr_epilogue(a, U, base, wl, n0, tid, nullptr);
+#endif
+
     }
 #ifdef RT_STAMPS
-    if (tid == 0 && a.stamps) atomicAdd(&a.stamps[7], 1ull);
+    if (tid == 0 && a.stamps) {
+        RT_MARK(6);
+        unsigned long long* e = a.stamps + (uint64_t)kStampRecWords * (uint64_t)u;
+        const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));     // HW_REG_HW_ID
+        const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11));   // HW_REG_XCC_ID
+        e[0] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+#pragma unroll
+        for (int i = 0; i < kStampMarks; ++i) e[1 + i] = tl[i];
+        e[1 + kStampMarks] = (unsigned long long)p | ((unsigned long long)L << 16) |
+                             ((unsigned long long)U.mode << 24) | ((unsigned long long)n0 << 32) |
+                             ((unsigned long long)(U.dst == kSelSnr) << 48);
+    }
 #endif
 }
 

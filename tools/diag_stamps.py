@@ -1,44 +1,111 @@
 #!/usr/bin/env python3
-"""Per-phase cycle breakdown of the cone kernel (diagnostic build).
+"""Per-unit phase timeline of the cone kernel (diagnostic build).
 
 Run on the GPU box after `make -C riptide_amd/csrc stamps`:
-    RIPTIDE_AMD_LIB=riptide_amd/libriptide_amd_stamps.so python tools/diag_stamps.py
-Phases (thread 0 of every workgroup, s_memtime deltas summed over units):
-  6 setup (unit descriptor, range tree, source rows), 0 LDS-DMA issue,
-  2 descriptor table, 1 DMA wait, 3 merge levels, 4 HBM store, 5 fused S/N
-  epilogue; slot 7 counts units.
+    RIPTIDE_AMD_LIB=riptide_amd/libriptide_amd_stamps.so python tools/diag_stamps.py [batch]
+Every work unit writes one record (thread 0, s_memtime marks, no atomics):
+start, setup done, fill issued, descriptor table built, fill landed, merge
+done, end.  Reported: mean cycles per phase by unit kind (whole / tile,
+final pass with the S/N epilogue or not), per-CU residency (how many units
+a CU holds over time) and the idle gaps between units on a CU.
 """
 import ctypes
 import json
 import os
 import sys
 
+import numpy as np
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
+
+MARKS = 11
+REC = MARKS + 2
+PHASES = ["setup", "issue", "desc", "wait", "merge", "tail"]
 
 
 def main():
     import torch
     from riptide_amd import _lib, engine
     L = _lib.load()
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     n = 1 << 23
     plan = engine.PeriodogramPlan.for_search(n, 256e-6, 0.1, 10.0, 240, 260, ducy_max=0.05)
     buf = (ctypes.c_uint64 * 8)()
-    _lib.check(L.rt_diag_stamps(buf, 1))     # allocates the device counters first
-    B = 4
+    _lib.check(L.rt_diag_stamps(buf, 1))     # allocates the device records
     x = torch.randn((B, n), device="cuda", dtype=torch.float32)
     out = plan.run(x)
     torch.cuda.synchronize()
     _lib.check(L.rt_diag_stamps(buf, 1))
     out = plan.run(x, out=out)
     torch.cuda.synchronize()
-    _lib.check(L.rt_diag_stamps(buf, 1))
-    names = ["dma_issue", "fill_wait", "desc_table", "merge", "store", "snr", "setup", "items"]
-    tot = sum(buf[i] for i in range(7))
-    res = {names[i]: buf[i] for i in range(8)}
-    res["fractions"] = {names[i]: round(buf[i] / tot, 4) for i in range(7)}
-    res["cycles_per_item"] = tot / max(1, buf[7])
-    print(json.dumps(res))
+    cap = 1 << 21
+    rec = np.zeros(cap * REC, dtype=np.uint64)
+    cnt = ctypes.c_uint64(0)
+    _lib.check(L.rt_diag_timeline(rec.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), cap, ctypes.byref(cnt)))
+    nrec = int(cnt.value)
+    e = rec[:nrec * REC].reshape(nrec, REC).astype(np.int64)
+    e = e[e[:, 1] != 0]                      # units that returned early write nothing
+    print(json.dumps(analyse(e)))
+
+
+def analyse(e):
+    hw = e[:, 0] & 0xFFFFFFFF
+    xcc = (e[:, 0] >> 32) & 0xF
+    cu = ((hw >> 8) & 0xF) | (((hw >> 12) & 1) << 4) | (((hw >> 13) & 0x7) << 5) | (xcc << 8)
+    t = e[:, 1:1 + MARKS]
+    tend = t[:, 6]
+    shape = e[:, 1 + MARKS]
+    snr = (shape >> 48) & 1
+    mode = (shape >> 24) & 0xFF
+    lv = (shape >> 16) & 0xFF
+    n0 = (shape >> 32) & 0xFFFF
+    ph = np.diff(t[:, :7], axis=1)
+    out = {"units": int(e.shape[0]), "distinct_cus": int(np.unique(cu).size),
+           "mean_cycles": dict(zip(PHASES, ph.mean(axis=0).round(0).tolist())),
+           "mean_total": float((tend - t[:, 0]).mean())}
+    groups = {}
+    for km in (0, 1):
+        for ks in (0, 1):
+            m = (mode == km) & (snr == ks)
+            if m.any():
+                g = {"units": int(m.sum()), "levels": round(float(lv[m].mean()), 2),
+                     "rows": round(float(n0[m].mean()), 1)}
+                g.update(dict(zip(PHASES, ph[m].mean(axis=0).round(0).tolist())))
+                groups[("whole" if km == 0 else "tile") + ("_snr" if ks else "")] = g
+    out["groups"] = groups
+    m = (snr == 1) & np.all(t[:, 7:11] > 0, axis=1)
+    if m.any():
+        sn = t[m]
+        out["snr_pass0"] = {"prefix": float((sn[:, 7] - sn[:, 5]).mean()), "barrier": float((sn[:, 8] - sn[:, 7]).mean()),
+                            "window": float((sn[:, 9] - sn[:, 8]).mean()), "widths": float((sn[:, 10] - sn[:, 9]).mean()),
+                            "rest": float((sn[:, 6] - sn[:, 10]).mean())}
+    # per-CU residency and idle gaps (s_memtime is per XCD: compare within a CU only)
+    occ = np.zeros(4)
+    gaps = []
+    for c in np.unique(cu):
+        m = cu == c
+        ev = np.concatenate([np.stack([t[m, 0], np.ones(m.sum())], 1), np.stack([tend[m], -np.ones(m.sum())], 1)])
+        ev = ev[np.lexsort((-ev[:, 1], ev[:, 0]))]
+        level, last, idle_from = 0, ev[0, 0], None
+        for tt, d in ev:
+            occ[min(int(level), 3)] += tt - last
+            if level == 0 and d > 0 and idle_from is not None:
+                gaps.append(tt - idle_from)
+            level += d
+            last = tt
+            if level == 0:
+                idle_from = tt
+    tot = occ.sum()
+    out["cu_residency_frac"] = {k: round(float(v / tot), 4) for k, v in zip(("0", "1", "2", "3+"), occ)}
+    gaps = np.array(gaps)
+    if gaps.size:
+        edges = [0, 2e3, 8e3, 32e3, 128e3, 1e12]
+        out["idle_gaps_count_cycles"] = {
+            f"<{edges[i + 1]:.0e}": [int(((gaps >= edges[i]) & (gaps < edges[i + 1])).sum()),
+                                      float(gaps[(gaps >= edges[i]) & (gaps < edges[i + 1])].sum())]
+            for i in range(len(edges) - 1)}
+    return out
 
 
 if __name__ == "__main__":
