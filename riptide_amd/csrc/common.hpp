@@ -30,8 +30,12 @@ namespace rt {
 // ---- cone kernel geometry (gfx950: 160 KiB LDS per CU).  512-thread
 // workgroups with ~77 KiB of LDS each, two per CU; the level buffer holds
 // dense rows (stride p).
-constexpr int kConeBlock = 512;             // 8 waves
+#ifndef RT_CONE_BLOCK
+#define RT_CONE_BLOCK 512
+#endif
+constexpr int kConeBlock = RT_CONE_BLOCK;   // 8 waves; two workgroups per CU (RT_CONE_BLOCK=1024: 16 waves, 64 VGPRs, measured slower)
 constexpr int kConeWaves = kConeBlock / 64;
+constexpr int kConeWavesPerSimd = 2 * kConeWaves / 4;
 constexpr int kLdsDataFloats = 17408;       // 68 KiB level buffer
 constexpr int kLdsPadFloats = 128;          // slack read (never used) by the unused slots of the last row
 constexpr int kMaxRows = 512;               // rows per level (source-row table, descriptors)
@@ -41,13 +45,17 @@ constexpr int kMaxLevels = 11;              // merge levels of any unit (whole u
 constexpr int kMaxRanges = (1 << (kMaxTileLevels + 1)) - 1;
 constexpr int kMaxWidths = 32;              // boxcar widths handled by the fused S/N epilogue
 constexpr int kSnrChunk = 17;               // S/N epilogue: columns per lane held in registers
-constexpr int kStageRegs = 45;              // merge: staged output values per lane (rows x slots)
+constexpr int kStageRegs = kConeBlock >= 1024 ? 25 : 45;   // merge: staged values per lane (rows x slots)
 constexpr int kMaxSlots = 45;               // merge: 64-bin slots per row (p <= 2880)
-constexpr int kMaxRowsPerWave = 24;         // merge: staged rows per wave (SGPR descriptors per row)
+constexpr int kMaxRowsPerWave = kConeBlock >= 1024 ? 12 : 24;   // merge: staged rows per wave
 // float4 chunks per thread of the fill: a level of n rows spans at most
 // n*p/4 + n aligned chunks (one extra per row for misalignment), n*p <=
 // kLdsDataFloats and n <= kMaxRows.
 constexpr int kFillChunks = (kLdsDataFloats / 4 + kMaxRows + kConeBlock - 1) / kConeBlock;
+
+// LDS row stride of a level of p-bin rows: even (8-byte aligned bin pairs)
+// and > p (column p holds a copy of column 0).
+RT_HD inline uint32_t row_stride(uint32_t p) { return (p + 2u) & ~1u; }
 
 // Merge variant for rows of p phase bins: slots per row rounded up to an
 // instantiated width (1..5, 8, 16, 45); 0 if p is too wide for the LDS engine.
@@ -64,7 +72,7 @@ RT_HD inline int merge_slots(uint32_t p)
 // Rows per wave the merge stages for a slot width (register budget).
 RT_HD constexpr int merge_rows_per_wave(int smax)
 {
-    return kStageRegs / smax < kMaxRowsPerWave ? kStageRegs / smax : kMaxRowsPerWave;
+    return kStageRegs / smax < 1 ? 1 : (kStageRegs / smax < kMaxRowsPerWave ? kStageRegs / smax : kMaxRowsPerWave);
 }
 
 // Row capacity of one cone work unit for p phase bins run by the kernel
@@ -73,7 +81,7 @@ RT_HD constexpr int merge_rows_per_wave(int smax)
 RT_HD inline int lds_row_capacity(uint32_t p, int smax)
 {
     if (!smax || p == 0) return 0;
-    int c = kLdsDataFloats / (int)p;
+    int c = kLdsDataFloats / (int)row_stride(p);
     const int stage = kConeWaves * merge_rows_per_wave(smax);
     if (stage < c) c = stage;
     return c < kMaxRows ? c : kMaxRows;
@@ -105,14 +113,11 @@ constexpr uint64_t kTimelineCap = 1u << 21;
 // cone kernel feature bits (ConeArgs::flags)
 enum : uint32_t {
     kConeStoreFromRegs = 1u,   // non-final passes store the output level straight from registers
-    kConeFuseLevels = 2u,      // two merge levels per LDS round trip
-    kConeFastMerge = 4u,       // SMAX <= 5 merge with per-row wrap-slot specialisation
-    kConeFillVec = 16u,        // fill lands aligned chunks with ds_write_b128
     kConeDiagNoSnr = 1u << 30, // diagnostics only (wrong results): skip the S/N epilogue
     kConeDiagNoMerge = 1u << 29, // diagnostics only (wrong results): skip the merge levels
     kConeDiagNoWrite = 1u << 28, // diagnostics only (wrong results): skip the level write-back
     kConeDiagNoBarrier = 1u << 27, // diagnostics only (wrong results): no barriers between merge levels
-    kConeDefaultFeatures = 17u
+    kConeDefaultFeatures = 1u
 };
 enum : uint8_t { kSelLeaves = 0, kSelPing = 1, kSelPong = 2, kSelSnr = 3 };
 

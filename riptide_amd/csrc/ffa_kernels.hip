@@ -293,9 +293,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* p, uin
     return __builtin_amdgcn_make_buffer_rsrc(uni_ptr(const_cast<void*>(p)), (short)0, uni((int)bytes), 0x00020000);
 }
 
-// Fill of a unit's bottom level: 16-byte aligned global loads into
-// registers (issued before the descriptor build, so their latency overlaps
-// it), then scattered element-wise into the dense LDS rows.  A whole unit is
+// ---- LDS level buffer: rows of stride q = row_stride(p) (even, > p).  Column
+// p of every row holds a copy of column 0, so the two-bin tail read of the
+// pair that straddles the roll's wrap point, (T[p-1], T[0]), is contiguous;
+// with q even, every pair (2i, 2i+1) of a row is 8-byte aligned.
+
+// Fill of a unit's bottom level into dense rows (stride p; the first merge
+// level re-strides to q): 16-byte aligned global loads into registers
+// (issued before the descriptor build, so their latency overlaps it), then
+// landed in LDS.  A whole unit is
 // one contiguous block of rows; a tile unit is read row by row (its rows come
 // from 2^L separate ranges).  Chunk k of a thread holds elements
 // e[k] .. e[k] + 3 of the LDS segment starting at lo[k]; elements outside
@@ -374,7 +380,7 @@ __device__ __forceinline__ void fill_issue(const ConeArgs& a, const UnitMeta& M,
 // 16-byte aligned and lies wholly inside its segment is one ds_write_b128
 // (8x8-lane groups over 32 banks: conflict-free); the others (segment ends,
 // tile rows of odd phase) are written element-wise.
-__device__ __forceinline__ void fill_land(const Fill& F, float* base, bool vec_ok)
+__device__ __forceinline__ void fill_land(const Fill& F, float* base)
 {
     const unsigned len = (unsigned)F.len;
     const int al = F.al;
@@ -382,7 +388,7 @@ __device__ __forceinline__ void fill_land(const Fill& F, float* base, bool vec_o
     for (int k = 0; k < kFillChunks; ++k) {
         const int e = F.e[k];
         float* row = base + F.lo[k];
-        const bool vec = vec_ok && e >= 0 && e + 3 < (int)len && ((F.lo[k] + e + al) & 3) == 0;
+        const bool vec = e >= 0 && e + 3 < (int)len && ((F.lo[k] + e + al) & 3) == 0;
         if (vec) {
             *reinterpret_cast<float4*>(row + e) = F.v[k];
         } else {
@@ -394,17 +400,11 @@ __device__ __forceinline__ void fill_land(const Fill& F, float* base, bool vec_o
     }
 }
 
-// LDS byte address of an LDS pointer.
-__device__ __forceinline__ uint32_t lds_addr(const float* p)
-{
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
-}
-
-
-// Row descriptor (LDS float offsets of the head and tail rows, roll shift) of
-// output row r at level l; to = -1 for a carried leaf (size-1 node).
-__device__ __forceinline__ void row_desc(const UnitMeta& M, bool tile, int node_size, int l, int r, int p, int& ho,
-                                         int& to, int& sh)
+// Row descriptor (head row, tail row, roll shift) of output row r at level
+// l, as row indices of the level below; t = -1 for a carried leaf (size-1
+// node).
+__device__ __forceinline__ void row_desc(const UnitMeta& M, bool tile, int node_size, int l, int r, int p, int& h,
+                                         int& t, int& sh)
 {
     if (tile) {
         const Range* lv = &M.ranges[(1 << l) - 1];
@@ -418,11 +418,11 @@ __device__ __forceinline__ void row_desc(const UnitMeta& M, bool tile, int node_
         const Range H = M.ranges[(2 << l) - 1 + 2 * lo];
         const Range T = M.ranges[(2 << l) + 2 * lo];
         const uint32_t hs = (uint32_t)R.size >> 1, ts = (uint32_t)R.size - hs;
-        const int h = (int)merge_index(merge_coef(hs, (uint32_t)R.size), (uint32_t)u);
-        const int t = (int)merge_index(merge_coef(ts, (uint32_t)R.size), (uint32_t)u);
-        ho = (H.base + h - H.lo) * p;
-        to = (T.base + t - T.lo) * p;
-        sh = (u - t) % p;
+        const int hh = (int)merge_index(merge_coef(hs, (uint32_t)R.size), (uint32_t)u);
+        const int tt = (int)merge_index(merge_coef(ts, (uint32_t)R.size), (uint32_t)u);
+        h = H.base + hh - H.lo;
+        t = T.base + tt - T.lo;
+        sh = (u - tt) % p;
     } else {
         int a0 = 0, sz = node_size;
         for (int d = 0; d < l; ++d) {
@@ -436,17 +436,17 @@ __device__ __forceinline__ void row_desc(const UnitMeta& M, bool tile, int node_
             }
         }
         if (sz <= 1) {
-            ho = r * p;
-            to = -1;
+            h = r;
+            t = -1;
             sh = 0;
         } else {
             const int s = r - a0;
             const uint32_t hs = (uint32_t)sz >> 1, ts = (uint32_t)sz - hs;
-            const int h = (int)merge_index(merge_coef(hs, (uint32_t)sz), (uint32_t)s);
-            const int t = (int)merge_index(merge_coef(ts, (uint32_t)sz), (uint32_t)s);
-            ho = (a0 + h) * p;
-            to = (a0 + (int)hs + t) * p;
-            sh = (s - t) % p;
+            const int hh = (int)merge_index(merge_coef(hs, (uint32_t)sz), (uint32_t)s);
+            const int tt = (int)merge_index(merge_coef(ts, (uint32_t)sz), (uint32_t)s);
+            h = a0 + hh;
+            t = a0 + (int)hs + tt;
+            sh = (s - tt) % p;
         }
     }
 }
@@ -455,10 +455,9 @@ __device__ __forceinline__ void row_desc(const UnitMeta& M, bool tile, int node_
 // kCarried: a size-1 node carried unchanged).  Rows < 1023, shift < 4096.
 constexpr uint32_t kCarried = 1023;
 
-__device__ __forceinline__ uint32_t pack_desc(int ho, int to, int sh, int p)
+__device__ __forceinline__ uint32_t pack_desc(int h, int t, int sh)
 {
-    const uint32_t h = (uint32_t)(ho / p), t = to < 0 ? kCarried : (uint32_t)(to / p);
-    return h | (t << 10) | ((uint32_t)sh << 20);
+    return (uint32_t)h | ((t < 0 ? kCarried : (uint32_t)t) << 10) | ((uint32_t)sh << 20);
 }
 
 // First table entry of level l: levels 0..l-1 precede it.
@@ -474,281 +473,310 @@ __device__ __forceinline__ void build_desc_table(const UnitMeta& M, uint32_t* de
             r -= uni(M.nrows[l]);
             ++l;
         }
-        int ho, to, sh;
-        row_desc(M, tile, node_size, l, r, p, ho, to, sh);
-        desc[idx] = pack_desc(ho, to, sh, p);
+        int h, t, sh;
+        row_desc(M, tile, node_size, l, r, p, h, t, sh);
+        desc[idx] = pack_desc(h, t, sh);
     }
 }
 
 typedef const __attribute__((address_space(3))) float* lds_cptr;
+typedef float lds_f2 __attribute__((ext_vector_type(2), aligned(8)));
+typedef const __attribute__((address_space(3))) lds_f2* lds_cptr2;
 
-// Outputs of level l (rows wave + 8i, bins lane + 64k) into v.  CARRIED:
-// the level may hold size-1 nodes (whole units near their leaves).
-template <int SMAX, int RW, bool CARRIED>
-__device__ __forceinline__ void merge_level(const UnitMeta& M, const float* data, const uint32_t* desc,
-                                            bool use_table, int p, int l, bool tile, int node_size, int lane,
-                                            int wave, int nr, float (&v)[RW][SMAX])
+// LDS reads the compiler must not pair into ds_read2_b32 / ds_read2st64_b64
+// (those issue at half the rate of separate ds_read_b32 / ds_read_b64 on
+// gfx950, tools/microbench/lds_b64.hip): volatile accesses are never merged.
+__device__ __forceinline__ float lds_ld(lds_cptr p) { return *(const volatile __attribute__((address_space(3))) float*)p; }
+__device__ __forceinline__ lds_f2 lds_ld2(lds_cptr2 p)
 {
-    const int S = (p + 63) >> 6;
-    int ho = 0, to = -1, sh = 0;
-    if (lane < nr) {
-        const int r = wave + kConeWaves * lane;
-        if (use_table) {
-            const uint32_t d = desc[desc_offset(M, l) + r];
-            const uint32_t t = (d >> 10) & 1023u;
-            ho = (int)(d & 1023u) * p;
-            to = t == kCarried ? -1 : (int)t * p;
-            sh = (int)(d >> 20);
-        } else {
-            row_desc(M, tile, node_size, l, r, p, ho, to, sh);
-        }
-    }
-    // Branch-free over rows and (narrow) slots, so the LDS reads of all the
-    // wave's rows are in flight together: rows i >= nr (descriptor of lane i:
-    // head row 0) and slots past p read in-bounds garbage that is never
-    // written back.  The rolled tail read of bin j = lane + 64k is
-    // T[j + s] or, past the wrap point (lane >= p - s - 64k), T[j + s - p]:
-    // two per-row base addresses and a compare/select per slot.  A carried
-    // leaf (to < 0) reads row 0 as its tail and adds -0.0 instead
-    // (x + (-0.0) == x exactly, as the reference's copy).
-#pragma unroll
-    for (int i = 0; i < RW; ++i) {
-        const int hb = __builtin_amdgcn_readlane(ho, i);
-        const int tb = __builtin_amdgcn_readlane(to, i);
-        const int s = __builtin_amdgcn_readlane(sh, i);
-        const float* hrow = data + hb + lane;
-        // T[j + s] and T[j + s - p]: two opaque LDS addresses, so each slot
-        // is one compare + one select, the slot offset 256k an immediate
-        lds_cptr ta = (lds_cptr)(data + (tb < 0 ? 0 : tb) + s + lane);
-        lds_cptr tw = ta - p;
-        asm("" : "+v"(ta), "+v"(tw));
-        const int thr = p - s;
-        uint32_t keep = 0xFFFFFFFFu, neg0 = 0u;
-        if (CARRIED) {
-            // a select on this uniform condition would become a branch per slot
-            keep = tb < 0 ? 0u : 0xFFFFFFFFu;
-            neg0 = ~keep & 0x80000000u;
-        }
-#pragma unroll
-        for (int k = 0; k < SMAX; ++k) {
-            if (SMAX <= 5 || k < S) {
-                const lds_cptr tp = lane >= thr - 64 * k ? tw : ta;
-                float t = tp[64 * k];
-                if (CARRIED) t = __uint_as_float((__float_as_uint(t) & keep) | neg0);
-                v[i][k] = __fadd_rn(hrow[64 * k], t);
-            }
-        }
-    }
+    return *(const volatile __attribute__((address_space(3))) lds_f2*)p;
 }
 
-// Level l without size-1 nodes, SMAX <= 5 slots (the hot path).  Per row the
-// descriptor is one v_readlane of the packed word (unpacked in SALU); the
-// head, tail and wrapped-tail rows are three VGPR bases (row base + 4 lane)
-// and the slot offsets 256k immediates.  The tail wraps inside slot
-// kw = (p - s) / 64: slots before it read T[j + s], slots after it
-// T[j + s - p], and only slot kw selects per lane -- a uniform switch on kw
-// picks the straight-line variant.
-template <int SMAX, int KW>
-__device__ __forceinline__ void merge_row_slots(lds_cptr hrow, lds_cptr ta, lds_cptr tw, int lane, int thr,
-                                                float (&v)[SMAX])
-{
-#pragma unroll
-    for (int k = 0; k < SMAX; ++k) {
-        float t;
-        if (k < KW) t = ta[64 * k];
-        else if (k > KW) t = tw[64 * k];
-        else t = (lane >= thr - 64 * k ? tw : ta)[64 * k];
-        v[k] = __fadd_rn(hrow[64 * k], t);
-    }
-}
-
-template <int SMAX, int KW>
-struct MergeRowSwitch {
-    __device__ static __forceinline__ void run(int kw, lds_cptr hrow, lds_cptr ta, lds_cptr tw, int lane, int thr,
-                                               float (&v)[SMAX])
-    {
-        if (kw == KW || KW == SMAX) merge_row_slots<SMAX, KW>(hrow, ta, tw, lane, thr, v);
-        else if constexpr (KW < SMAX) MergeRowSwitch<SMAX, KW + 1>::run(kw, hrow, ta, tw, lane, thr, v);
-    }
+// Register layout of one row of a level (SMAX 64-bin half-slots):
+// pair slot k < NP holds bins 2 lane + 128k and 2 lane + 128k + 1 in
+// v[2k], v[2k+1]; with SMAX odd, a single slot holds bin 128 NP + lane in
+// v[2 NP].
+template <int SMAX>
+struct RowLayout {
+    static constexpr int NP = SMAX / 2;
+    static constexpr bool SG = (SMAX & 1) != 0;
 };
 
-template <int SMAX, int RW>
-__device__ __forceinline__ void merge_level_fast(const UnitMeta& M, const float* data, const uint32_t* desc,
-                                                 bool use_table, int p, int l, bool tile, int node_size, int lane,
-                                                 int wave, int nr, float (&v)[RW][SMAX])
+// Outputs of level l (rows wave + 8i) into v.
+//   out[j] = H[j] + T[(j + s) mod p]
+// Per row the descriptor is one v_readlane of the packed word (unpacked in
+// SALU).  A pair slot is one ds_read_b64 of H (aligned) and two ds_read_b32
+// of T at one address: T[j + s] before the wrap point p - s, T[j + s - p]
+// from it on (two opaque per-row bases and a compare/select per slot; the
+// pair straddling the wrap point reads the column-0 copy).  The additions
+// are the reference's, element by element.  CARRIED: the level may hold
+// size-1 nodes (whole units near their leaves), whose rows add -0.0 to H
+// (x + (-0.0) == x exactly, as the reference's copy).  Branch-free over rows
+// and slots: rows i >= nr and bins past p read in-bounds garbage that is
+// never written back.
+template <int SMAX, int RW, bool CARRIED>
+__device__ __forceinline__ void merge_level(const UnitMeta& M, const float* data, const uint32_t* desc,
+                                            bool use_table, int p, int q, int l, bool tile, int node_size, int lane,
+                                            int wave, int nr, float (&v)[RW][SMAX])
 {
-    static_assert(SMAX <= 5, "fast merge: SMAX <= 5");
+    constexpr int NP = RowLayout<SMAX>::NP;
+    constexpr bool SG = RowLayout<SMAX>::SG;
+    const int S2 = (p + 127) >> 7;                      // pair slots holding bins
     uint32_t d = 0;
     if (lane < nr) {
         const int r = wave + kConeWaves * lane;
         if (use_table) {
             d = desc[desc_offset(M, l) + r];
         } else {
-            int ho, to, sh;
-            row_desc(M, tile, node_size, l, r, p, ho, to, sh);
-            d = pack_desc(ho, to, sh, p);
+            int h, t, sh;
+            row_desc(M, tile, node_size, l, r, p, h, t, sh);
+            d = pack_desc(h, t, sh);
         }
     }
-    const lds_cptr lbase = (lds_cptr)data + lane;
+    const lds_cptr l2 = (lds_cptr)data + 2 * lane;
+    const lds_cptr l1 = (lds_cptr)data + lane;
+    const int lane2 = 2 * lane;
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
-        if (i < nr) {
-            const uint32_t dw = (uint32_t)__builtin_amdgcn_readlane((int)d, i);
-            const int h = (int)(dw & 1023u), t = (int)((dw >> 10) & 1023u), sft = (int)(dw >> 20);
-            lds_cptr hrow = lbase + h * p;
-            lds_cptr ta = lbase + (t * p + sft);
-            lds_cptr tw = lbase + (t * p + sft - p);
-            asm("" : "+v"(ta), "+v"(tw));
-            const int thr = p - sft;
-            MergeRowSwitch<SMAX, 0>::run(thr >> 6, hrow, ta, tw, lane, thr, v[i]);
+        const uint32_t dw = (uint32_t)__builtin_amdgcn_readlane((int)d, i);
+        const int h = (int)(dw & 1023u), sft = (int)(dw >> 20);
+        const uint32_t tc = (dw >> 10) & 1023u;
+        const int t = tc == kCarried ? 0 : (int)tc;
+        uint32_t keep = 0xFFFFFFFFu, neg0 = 0u;
+        if (CARRIED) {
+            keep = tc == kCarried ? 0u : 0xFFFFFFFFu;
+            neg0 = ~keep & 0x80000000u;
         }
-    }
-}
-
-// Descriptor (LDS float offsets of head and tail rows, shift; tail -1 when
-// carried) of output row r of level l, from the table or computed.
-__device__ __forceinline__ void level_desc(const UnitMeta& M, const uint32_t* desc, bool use_table, int p, int l,
-                                           int r, bool tile, int node_size, int& ho, int& to, int& sh)
-{
-    if (use_table) {
-        const uint32_t d = desc[desc_offset(M, l) + r];
-        const uint32_t t = (d >> 10) & 1023u;
-        ho = (int)(d & 1023u) * p;
-        to = t == kCarried ? -1 : (int)t * p;
-        sh = (int)(d >> 20);
-    } else {
-        row_desc(M, tile, node_size, l, r, p, ho, to, sh);
-    }
-}
-
-// Two merge levels at once: outputs of level l (rows wave + 8i) from the rows
-// of level l + 2 in LDS, into v.  With H = HH + roll(HT, sh) and
-// T = TH + roll(TT, st) the level l + 1 rows of output row r:
-//     out[j] = (HH[j] + HT[j + sh]) + (TH[j + s1] + TT[j + s1 + st])   (mod p)
-// -- exactly the reference's additions, without writing level l + 1 back to
-// LDS.  A carried (size-1) node contributes -0.0 (x + (-0.0) == x).
-template <int SMAX, int RW>
-__device__ __forceinline__ void merge_level2(const UnitMeta& M, const float* data, const uint32_t* desc,
-                                             bool use_table, int p, int l, bool tile, int node_size, int lane,
-                                             int wave, int nr, float (&v)[RW][SMAX])
-{
-    const int S = (p + 63) >> 6;
-    int hh = 0, ht = 0, th = 0, tt = 0, sh = 0, s1 = 0, s13 = 0, flags = 0;
-    if (lane < nr) {
-        const int r = wave + kConeWaves * lane;
-        int ho, to;
-        level_desc(M, desc, use_table, p, l, r, tile, node_size, ho, to, s1);
-        int a, b, sa;
-        level_desc(M, desc, use_table, p, l + 1, ho / p, tile, node_size, a, b, sa);
-        hh = a;
-        ht = b < 0 ? 0 : b;
-        sh = sa;
-        flags = b < 0 ? 1 : 0;                     // HT carried
-        if (to < 0) {
-            flags |= 2;                            // whole tail carried
-        } else {
-            int c, d, sc;
-            level_desc(M, desc, use_table, p, l + 1, to / p, tile, node_size, c, d, sc);
-            th = c;
-            tt = d < 0 ? 0 : d;
-            s13 = s1 + sc >= p ? s1 + sc - p : s1 + sc;
-            if (d < 0) flags |= 4;                 // TT carried
+        const int thr = p - sft;
+        const lds_cptr2 hrow2 = (lds_cptr2)(l2 + h * q);
+        lds_cptr ta2 = l2 + (t * q + sft);
+        lds_cptr tw2 = ta2 - p;
+        asm("" : "+v"(ta2), "+v"(tw2));
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            if (SMAX <= 5 || k < S2) {
+                const lds_cptr tp = lane2 >= thr - 128 * k ? tw2 : ta2;
+                float x0 = lds_ld(tp + 128 * k), x1 = lds_ld(tp + 128 * k + 1);
+                if (CARRIED) {
+                    x0 = __uint_as_float((__float_as_uint(x0) & keep) | neg0);
+                    x1 = __uint_as_float((__float_as_uint(x1) & keep) | neg0);
+                }
+                const lds_f2 hv = lds_ld2(hrow2 + 64 * k);
+                v[i][2 * k] = __fadd_rn(hv.x, x0);
+                v[i][2 * k + 1] = __fadd_rn(hv.y, x1);
+            }
         }
-    }
-#pragma unroll
-    for (int i = 0; i < RW; ++i) {
-        const int bhh = __builtin_amdgcn_readlane(hh, i);
-        const int bht = __builtin_amdgcn_readlane(ht, i);
-        const int bth = __builtin_amdgcn_readlane(th, i);
-        const int btt = __builtin_amdgcn_readlane(tt, i);
-        const int ssh = __builtin_amdgcn_readlane(sh, i);
-        const int ss1 = __builtin_amdgcn_readlane(s1, i);
-        const int ss13 = __builtin_amdgcn_readlane(s13, i);
-        const int fl = __builtin_amdgcn_readlane(flags, i);
-        const uint32_t k_ht = (fl & 1) ? 0u : 0xFFFFFFFFu;
-        const uint32_t k_th = (fl & 2) ? 0u : 0xFFFFFFFFu;
-        const uint32_t k_tt = (fl & 6) ? 0u : 0xFFFFFFFFu;
-        const float* r_hh = data + bhh + lane;
-        const float* r_ht = data + bht;
-        const float* r_th = data + bth;
-        const float* r_tt = data + btt;
-#pragma unroll
-        for (int k = 0; k < SMAX; ++k) {
-            if (SMAX <= 5 || k < S) {
-                const uint32_t j = (uint32_t)(lane + 64 * k);
-                const uint32_t ca = j + (uint32_t)ssh, cb = j + (uint32_t)ss1, cc = j + (uint32_t)ss13;
-                const float x_hh = r_hh[64 * k];
-                const float x_ht = __uint_as_float((__float_as_uint(r_ht[min(ca, ca - (uint32_t)p)]) & k_ht) |
-                                                   (~k_ht & 0x80000000u));
-                const float x_th = __uint_as_float((__float_as_uint(r_th[min(cb, cb - (uint32_t)p)]) & k_th) |
-                                                   (~k_th & 0x80000000u));
-                const float x_tt = __uint_as_float((__float_as_uint(r_tt[min(cc, cc - (uint32_t)p)]) & k_tt) |
-                                                   (~k_tt & 0x80000000u));
-                v[i][k] = __fadd_rn(__fadd_rn(x_hh, x_ht), __fadd_rn(x_th, x_tt));
+        if constexpr (SG) {
+            if (SMAX <= 5 || p > 128 * NP) {
+                const lds_cptr hrow1 = l1 + h * q;
+                lds_cptr ta1 = l1 + (t * q + sft);
+                lds_cptr tw1 = ta1 - p;
+                asm("" : "+v"(ta1), "+v"(tw1));
+                const lds_cptr tp = lane >= thr - 128 * NP ? tw1 : ta1;
+                float x = lds_ld(tp + 128 * NP);
+                if (CARRIED) x = __uint_as_float((__float_as_uint(x) & keep) | neg0);
+                v[i][2 * NP] = __fadd_rn(lds_ld(hrow1 + 128 * NP), x);
             }
         }
     }
 }
 
-// All merge levels of one unit, two at a time where possible (a single level
-// first when L is odd).  SMAX >= ceil(p/64) slots per row, RW rows per wave
-// (lds_row_capacity(p, SMAX) guarantees ceil(rows/8) <= RW at every level).
-// With `st` set (a non-final pass), the output level goes from the staging
-// registers straight to global memory at byte offset st_o0 (rows of the tile
-// are one contiguous segment) instead of back into LDS.
+// The unit's first merge level, reading the filled level in its dense layout
+// (rows of stride p at `src`): bins j = lane + 64k, one ds_read_b32 of H and
+// one of T per slot (T[j + s] before the wrap point p - s, T[j + s - p] from
+// it on: two opaque per-row bases and a compare/select per slot).  The
+// outputs go to v in the same lane + 64k layout; the write-back re-strides
+// them to q.
+template <int SMAX, int RW, bool CARRIED>
+__device__ __forceinline__ void merge_level_dense(const UnitMeta& M, const float* src, const uint32_t* desc,
+                                                  bool use_table, int p, int l, bool tile, int node_size, int lane,
+                                                  int wave, int nr, float (&v)[RW][SMAX])
+{
+    const int S = (p + 63) >> 6;
+    uint32_t d = 0;
+    if (lane < nr) {
+        const int r = wave + kConeWaves * lane;
+        if (use_table) {
+            d = desc[desc_offset(M, l) + r];
+        } else {
+            int h, t, sh;
+            row_desc(M, tile, node_size, l, r, p, h, t, sh);
+            d = pack_desc(h, t, sh);
+        }
+    }
+    const lds_cptr l1 = (lds_cptr)src + lane;
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+        const uint32_t dw = (uint32_t)__builtin_amdgcn_readlane((int)d, i);
+        const int h = (int)(dw & 1023u), sft = (int)(dw >> 20);
+        const uint32_t tc = (dw >> 10) & 1023u;
+        const int t = tc == kCarried ? 0 : (int)tc;
+        uint32_t keep = 0xFFFFFFFFu, neg0 = 0u;
+        if (CARRIED) {
+            keep = tc == kCarried ? 0u : 0xFFFFFFFFu;
+            neg0 = ~keep & 0x80000000u;
+        }
+        const lds_cptr hrow = l1 + h * p;
+        lds_cptr ta = l1 + (t * p + sft);
+        lds_cptr tw = ta - p;
+        asm("" : "+v"(ta), "+v"(tw));
+        const int thr = p - sft;
+#pragma unroll
+        for (int k = 0; k < SMAX; ++k) {
+            if (SMAX <= 5 || k < S) {
+                const lds_cptr tp = lane >= thr - 64 * k ? tw : ta;
+                float x = lds_ld(tp + 64 * k);
+                if (CARRIED) x = __uint_as_float((__float_as_uint(x) & keep) | neg0);
+                v[i][k] = __fadd_rn(lds_ld(hrow + 64 * k), x);
+            }
+        }
+    }
+}
+
+// All merge levels of one unit, deepest first.  SMAX >= ceil(p/64)
+// half-slots per row, RW rows per wave (lds_row_capacity(p, SMAX) guarantees
+// ceil(rows/8) <= RW at every level).  Each level's outputs are staged in
+// registers between two barriers (in-place update), then written back as
+// ds_write_b64 pairs (+ the single slot and the column-0 copy).  With `st`
+// set (a non-final pass), the output level goes from the staging registers
+// straight to global memory at byte offset st_o0 (rows of the tile are one
+// contiguous segment) instead of back into LDS.
+// Output level l == 0 of a non-final pass: straight from the staging
+// registers to global memory at byte offset st_o0 (the tile's rows are one
+// contiguous segment).  DENSE: registers hold bins lane + 64k, else the pair
+// layout.
+template <int SMAX, int RW, bool DENSE>
+__device__ __forceinline__ void store_rows(const float (&v)[RW][SMAX], int p, int lane, int wave, int nr,
+                                           __amdgpu_buffer_rsrc_t rs, uint32_t st_o0)
+{
+    constexpr int NP = RowLayout<SMAX>::NP;
+    constexpr bool SG = RowLayout<SMAX>::SG;
+    const int S = (p + 63) >> 6, S2 = (p + 127) >> 7;
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+        if (i < nr) {
+            const uint32_t ob = st_o0 + (uint32_t)((wave + kConeWaves * i) * p) * 4u;
+            if constexpr (DENSE) {
+#pragma unroll
+                for (int k = 0; k < SMAX; ++k)
+                    if ((SMAX <= 5 || k < S) && lane + 64 * k < p)
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs,
+                                                              (int)(ob + (uint32_t)(lane + 64 * k) * 4u), 0, 0);
+            } else {
+#pragma unroll
+                for (int k = 0; k < NP; ++k) {
+                    if (SMAX <= 5 || k < S2) {
+                        const int j = 2 * lane + 128 * k;
+                        const uint32_t o = ob + (uint32_t)j * 4u;
+                        if (128 * (k + 1) <= p) {
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][2 * k]), rs, (int)o, 0, 0);
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][2 * k + 1]), rs, (int)o + 4, 0,
+                                                                  0);
+                        } else {
+                            if (j < p)
+                                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][2 * k]), rs, (int)o, 0, 0);
+                            if (j + 1 < p)
+                                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][2 * k + 1]), rs, (int)o + 4,
+                                                                      0, 0);
+                        }
+                    }
+                }
+                if constexpr (SG) {
+                    if (lane + 128 * NP < p)
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][2 * NP]), rs,
+                                                              (int)(ob + (uint32_t)(lane + 128 * NP) * 4u), 0, 0);
+                }
+            }
+        }
+    }
+}
+
+// Write-back of a level's staged rows into LDS rows of stride q (+ the
+// column-0 copy): DENSE registers as one ds_write_b32 per slot, the pair
+// layout as ds_write_b64 pairs and the single slot.
+template <int SMAX, int RW, bool DENSE>
+__device__ __forceinline__ void write_rows(float* data, const float (&v)[RW][SMAX], int p, int q, int lane, int wave,
+                                           int nr)
+{
+    constexpr int NP = RowLayout<SMAX>::NP;
+    constexpr bool SG = RowLayout<SMAX>::SG;
+    const int S = (p + 63) >> 6, S2 = (p + 127) >> 7;
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+        if (i < nr) {
+            float* orow = data + (wave + kConeWaves * i) * q;
+            if constexpr (DENSE) {
+#pragma unroll
+                for (int k = 0; k < SMAX; ++k) {
+                    if (64 * (k + 1) <= p) orow[lane + 64 * k] = v[i][k];      // full slot: no lane mask
+                    else if ((SMAX <= 5 || k < S) && lane + 64 * k < p) orow[lane + 64 * k] = v[i][k];
+                }
+            } else {
+                float* o2 = orow + 2 * lane;
+#pragma unroll
+                for (int k = 0; k < NP; ++k) {
+                    if (SMAX <= 5 || k < S2) {
+                        // the pair (p-1, p) of an odd p writes column p; the copy below overwrites it
+                        if (128 * (k + 1) <= p || 2 * lane + 128 * k < p)
+                            *reinterpret_cast<float2*>(o2 + 128 * k) = make_float2(v[i][2 * k], v[i][2 * k + 1]);
+                    }
+                }
+                if constexpr (SG) {
+                    if (lane + 128 * NP < p) orow[lane + 128 * NP] = v[i][2 * NP];
+                }
+            }
+            if (lane == 0) orow[p] = v[i][0];           // column-0 copy (bin 0: lane 0, slot 0 in both layouts)
+        }
+    }
+}
+
+// All merge levels of one unit, deepest first.  SMAX >= ceil(p/64)
+// half-slots per row, RW rows per wave (lds_row_capacity(p, SMAX) guarantees
+// ceil(rows/8) <= RW at every level).  The first level reads the filled
+// (dense, stride p) level at `base`; every level's outputs are staged in
+// registers between two barriers (in-place update) and written back in
+// rows of stride q at `data`, where the next levels read them in the pair
+// layout.  With `st` set (a non-final pass), the output level goes from the
+// staging registers straight to global memory instead of back into LDS.
 template <int SMAX, int RW>
-__device__ __forceinline__ void merge_levels(const UnitMeta& M, float* data, const uint32_t* desc, bool use_table,
-                                             int p, int L, bool tile, int node_size, int tid, bool st,
-                                             __amdgpu_buffer_rsrc_t rs, uint32_t st_o0, bool fuse, uint32_t diag)
+__device__ __forceinline__ void merge_levels(const UnitMeta& M, float* data, const float* base, const uint32_t* desc,
+                                             bool use_table, int p, int q, int L, bool tile, int node_size, int tid,
+                                             bool st, __amdgpu_buffer_rsrc_t rs, uint32_t st_o0, uint32_t diag)
 {
     const int lane = tid & 63, wave = tid >> 6;
-    const int S = (p + 63) >> 6;
-    int top = L;                  // level held in LDS
-    while (top > 0) {
-        const bool two = fuse && top >= 2 && !((top & 1) && top == L);
-        const int l = two ? top - 2 : top - 1;
+    {
+        const int l = L - 1;
         const int orows = uni(M.nrows[l]);
         const int nr = uni(orows > wave ? (orows - wave + kConeWaves - 1) / kConeWaves : 0);
         float v[RW][SMAX];
         // size-1 nodes exist at depth l only in whole units with node_size >> l < 2
-        const bool carried = !tile && (node_size >> l) < 2;
-        if (two) merge_level2<SMAX, RW>(M, data, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
-        else if (carried) merge_level<SMAX, RW, true>(M, data, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
-        else if (SMAX <= 5 && (diag & kConeFastMerge)) {
-            if constexpr (SMAX <= 5)
-                merge_level_fast<SMAX, RW>(M, data, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
-        } else merge_level<SMAX, RW, false>(M, data, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
+        if (!tile && (node_size >> l) < 2)
+            merge_level_dense<SMAX, RW, true>(M, base, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
+        else
+            merge_level_dense<SMAX, RW, false>(M, base, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
         if (l == 0 && st) {
-#pragma unroll
-            for (int i = 0; i < RW; ++i) {
-                if (i < nr) {
-                    const uint32_t o = st_o0 + (uint32_t)((wave + kConeWaves * i) * p + lane) * 4u;
-#pragma unroll
-                    for (int k = 0; k < SMAX; ++k)
-                        if (k < S && lane + 64 * k < p)
-                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs,
-                                                                  (int)(o + 256u * (uint32_t)k), 0, 0);
-                }
-            }
+            store_rows<SMAX, RW, true>(v, p, lane, wave, nr, rs, st_o0);
             return;
         }
         if (!(diag & kConeDiagNoBarrier)) lds_barrier();
-        if (diag & kConeDiagNoWrite) {
-        } else {
-#pragma unroll
-            for (int i = 0; i < RW; ++i) {
-                if (i < nr) {
-                    float* orow = data + (wave + kConeWaves * i) * p + lane;
-#pragma unroll
-                    for (int k = 0; k < SMAX; ++k) {
-                        if (64 * (k + 1) <= p) orow[64 * k] = v[i][k];            // full slot: no lane mask
-                        else if (k < S && lane + 64 * k < p) orow[64 * k] = v[i][k];
-                    }
-                }
-            }
+        if (!(diag & kConeDiagNoWrite)) write_rows<SMAX, RW, true>(data, v, p, q, lane, wave, nr);
+        if (!(diag & kConeDiagNoBarrier)) lds_barrier();
+    }
+    for (int l = L - 2; l >= 0; --l) {
+        const int orows = uni(M.nrows[l]);
+        const int nr = uni(orows > wave ? (orows - wave + kConeWaves - 1) / kConeWaves : 0);
+        float v[RW][SMAX];
+        if (!tile && (node_size >> l) < 2)
+            merge_level<SMAX, RW, true>(M, data, desc, use_table, p, q, l, tile, node_size, lane, wave, nr, v);
+        else
+            merge_level<SMAX, RW, false>(M, data, desc, use_table, p, q, l, tile, node_size, lane, wave, nr, v);
+        if (l == 0 && st) {
+            store_rows<SMAX, RW, false>(v, p, lane, wave, nr, rs, st_o0);
+            return;
         }
         if (!(diag & kConeDiagNoBarrier)) lds_barrier();
-        top = l;
+        if (!(diag & kConeDiagNoWrite)) write_rows<SMAX, RW, false>(data, v, p, q, lane, wave, nr);
+        if (!(diag & kConeDiagNoBarrier)) lds_barrier();
     }
 }
 
@@ -763,6 +791,9 @@ __device__ __forceinline__ void merge_levels(const UnitMeta& M, float* data, con
 // every width w <= kSnrWin from registers.  Wider rows and wider widths use
 // the general path (shuffles, LDS reads per width).
 constexpr int kSnrWin = 12;
+// S/N chunk columns per lane held in registers (and the window path), by the
+// register budget of the block size
+constexpr int kSnrMaxChunk = kConeBlock >= 1024 ? 9 : 17;
 
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v)
@@ -780,19 +811,34 @@ __device__ __forceinline__ double dpp_d(double v)
 
 // row_shr:d within 16-lane rows: lane g (of a G-lane group, G <= 16) takes
 // lane g - d of its group when g >= d.
-template <int G>
-__device__ __forceinline__ double seg_scan_dpp(double v, int g)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_d_rows(double v)
 {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROWS, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROWS, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
+// Inclusive scan over each G-lane group (G = 8 .. 64): row_shr steps inside
+// 16-lane rows, then row_bcast:15 / row_bcast:31 across rows.  The partial
+// sums start at +0.0 and are never -0.0, so adding the +0.0 that masked
+// lanes receive is an exact no-op.
+template <int G>
+__device__ __forceinline__ double seg_scan_dpp(double v, int lane)
+{
+    const int g = lane & (G < 16 ? G - 1 : 15);     // position inside the group's part of the 16-lane row
     double y = dpp_d<0x111>(v);
     v = g >= 1 ? v + y : v;
     y = dpp_d<0x112>(v);
     v = g >= 2 ? v + y : v;
     y = dpp_d<0x114>(v);
     v = g >= 4 ? v + y : v;
-    if (G == 16) {
+    if (G >= 16) {
         y = dpp_d<0x118>(v);
         v = g >= 8 ? v + y : v;
     }
+    if (G >= 32) v = v + dpp_d_rows<0x142, 0xA>(v);   // rows 1, 3 += lane 15 of rows 0, 2
+    if (G >= 64) v = v + dpp_d_rows<0x143, 0xC>(v);   // rows 2, 3 += lane 31
     return v;
 }
 
@@ -804,17 +850,26 @@ __device__ __forceinline__ float dpp_keep(float v)
     return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
 
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_keep_rows(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, ROWS, 0xF, false));
+}
+
 // max over the G lanes of a group, valid in lane g == G - 1.  fmaxf never
 // returns a NaN operand over a number, as diff_max's comparison.
 template <int G>
-__device__ __forceinline__ float seg_max_dpp(float v, int g)
+__device__ __forceinline__ float seg_max_dpp(float v, int lane)
 {
-    if constexpr (G == 16) {
+    if constexpr (G >= 16) {
         v = fmaxf(v, dpp_keep<0x111>(v));
         v = fmaxf(v, dpp_keep<0x112>(v));
         v = fmaxf(v, dpp_keep<0x114>(v));
         v = fmaxf(v, dpp_keep<0x118>(v));
+        if (G >= 32) v = fmaxf(v, dpp_keep_rows<0x142, 0xA>(v));
+        if (G >= 64) v = fmaxf(v, dpp_keep_rows<0x143, 0xC>(v));
     } else {
+        const int g = lane & 7;
         float y = dpp_keep<0x111>(v);
         v = g >= 1 ? fmaxf(v, y) : v;
         y = dpp_keep<0x112>(v);
@@ -856,10 +911,10 @@ struct WindowSwitch {
 #endif
 
 template <int CH, int G>
-__device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, float* data, const int* wl, int nev,
-                                         int c, int tid, unsigned long long* tl)
+__device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, float* data, int q, const int* wl,
+                                         int nev, int c, int tid, unsigned long long* tl)
 {
-    constexpr bool kDpp = G <= 16;
+    constexpr bool kDpp = true;
     const int lane = tid & 63;
     const int p = U.p;
     const int g = lane & (G - 1);
@@ -873,7 +928,7 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
     for (int base = 0; base < nev; base += rows_per_pass) {
         const int r = base + (tid / G);
         const bool active = r < nev;
-        float* row = data + min(r, nev - 1) * p + j0;
+        float* row = data + min(r, nev - 1) * q + j0;
         float cp[CH];
         // every lane reads CH columns at immediate offsets (past its chunk:
         // the next chunk, the next row or the LDS pad), masked to 0
@@ -889,8 +944,8 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
         for (int i = 0; i < CH; ++i) part = part + (double)cp[i];
         double acc;
         if constexpr (kDpp) {
-            const double incl = seg_scan_dpp<G>(part, g);
-            acc = dpp_d<0x111>(incl);
+            const double incl = seg_scan_dpp<G>(part, lane);
+            acc = dpp_d<0x138>(incl);               // wave_shr:1 -- lane g takes lane g - 1
         } else {
             double incl = part;
             for (int d = 1; d < G; d <<= 1) {
@@ -916,81 +971,82 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
         RT_SNR_MARK(7);
         lds_barrier();                        // prefix rows visible to all lanes
         RT_SNR_MARK(8);
-        const float* crow = data + min(r, nev - 1) * p;
-        float z[CH + kSnrWin];                // c[j0 + k], wrap c[p + j] = c[j] + sum applied
-        bool have_z = false;
-        for (uint32_t iw = 0; iw < nw; ++iw) {
-            const int w = uni(wl[iw]);
-            float dmax;
-            if (kDpp && w <= kSnrWin) {
-                if (!have_z) {
-                    // two opaque bases (row and row - p), slot offsets immediate
-                    lds_cptr za = (lds_cptr)(crow + j0);
-                    lds_cptr zb = za - p;
-                    asm("" : "+v"(za), "+v"(zb));
-#pragma unroll
-                    for (int k = 0; k < CH + kSnrWin; ++k) {
-                        const bool wrap = j0 + k >= p;
-                        const float va = za[k], vb = zb[k];
-                        z[k] = wrap ? __fadd_rn(vb, sum) : va;
-                    }
-                    have_z = true;
-                    RT_SNR_MARK(9);
-                }
-                dmax = WindowSwitch<CH, 1>::run(w, z, cp);
-            } else {
-                dmax = -INFINITY;
-                const int last = max(cnt - 1, 0);
-                float lv[CH];
-#pragma unroll
-                for (int t = 0; t < CH; ++t) {
-                    const int k = j0 + min(t, last) + w;
-                    lv[t] = crow[k >= p ? k - p : k];
-                }
-#pragma unroll
-                for (int i = 0; i < CH; ++i) {
-                    const bool wrap = j0 + min(i, last) + w >= p;
-                    const float ck = wrap ? __fadd_rn(lv[i], sum) : lv[i];
-                    dmax = fmaxf(dmax, __fsub_rn(ck, cp[i]));  // diff_max, kernels.hpp:50-60
-                }
-            }
-            if constexpr (kDpp) {
-                dmax = seg_max_dpp<G>(dmax, g);
-            } else {
-                for (int o = G >> 1; o > 0; o >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, o, G));
-            }
+        const float* crow = data + min(r, nev - 1) * q;
+        auto emit = [&](uint32_t iw, int w, float dmax) {
+            dmax = seg_max_dpp<G>(dmax, lane);
             if (active && g == writer) {
                 const float h = sqrtf((float)(p - w) / (float)(p * w));
                 const float b = (float)w / (float)(p - w) * h;
                 snr[(uint64_t)r * nw + iw] = ((h + b) * dmax - b * sum) / U.stdnoise;
             }
+        };
+        if constexpr (CH <= kSnrMaxChunk) {
+            // widths <= kSnrWin from the register window c[j0 .. j0 + CH + kSnrWin)
+            float z[CH + kSnrWin];
+            {
+                // two opaque bases (row and row - p), slot offsets immediate
+                lds_cptr za = (lds_cptr)(crow + j0);
+                lds_cptr zb = za - p;
+                asm("" : "+v"(za), "+v"(zb));
+#pragma unroll
+                for (int k = 0; k < CH + kSnrWin; ++k) {
+                    const bool wrap = j0 + k >= p;
+                    const float va = za[k], vb = zb[k];
+                    z[k] = wrap ? __fadd_rn(vb, sum) : va;
+                }
+            }
+            RT_SNR_MARK(9);
+            for (uint32_t iw = 0; iw < nw; ++iw) {
+                const int w = uni(wl[iw]);
+                if (w <= kSnrWin) emit(iw, w, WindowSwitch<CH, 1>::run(w, z, cp));
+            }
+        }
+        // wider widths: the window c[j0 + w ..] read from LDS per width
+        for (uint32_t iw = 0; iw < nw; ++iw) {
+            const int w = uni(wl[iw]);
+            if (CH <= kSnrMaxChunk && w <= kSnrWin) continue;
+            float dmax = -INFINITY;
+            const int last = max(cnt - 1, 0);
+            float lv[CH];
+#pragma unroll
+            for (int t = 0; t < CH; ++t) {
+                const int k = j0 + min(t, last) + w;
+                lv[t] = crow[k >= p ? k - p : k];
+            }
+#pragma unroll
+            for (int i = 0; i < CH; ++i) {
+                const bool wrap = j0 + min(i, last) + w >= p;
+                const float ck = wrap ? __fadd_rn(lv[i], sum) : lv[i];
+                dmax = fmaxf(dmax, __fsub_rn(ck, cp[i]));  // diff_max, kernels.hpp:50-60
+            }
+            emit(iw, w, dmax);
         }
         RT_SNR_MARK(10);
     }
 }
 
-__device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& U, float* data, const int* wl, int nrows,
-                                             int tid, unsigned long long* tl)
+__device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& U, float* data, int q, const int* wl,
+                                             int nrows, int tid, unsigned long long* tl)
 {
     const int lane = tid & 63, wave = tid >> 6;
     const int p = U.p;
     const int nev = (int)min((int64_t)nrows, (int64_t)U.rows_eval - (int64_t)U.s0);
     if (nev <= 0) return;
+    // G lanes per row: the smallest power of two >= 8 whose chunks fit
+    // kSnrMaxChunk columns (17 at G = 64); chunk lengths odd
     int G = 8;
-    while (G < 64 && ((((p + G - 1) / G) | 1) > kSnrChunk)) G <<= 1;
+    while (G < 64 && (((p + G - 1) / G) | 1) > kSnrMaxChunk) G <<= 1;
     int c = (p + G - 1) / G;
     if (c < kSnrChunk) c |= 1;
     const uint32_t nw = a.num_widths;
     float* snr = a.snr + (uint64_t)U.trial * a.snr_stride + (U.snr_row + (uint64_t)U.s0) * (uint64_t)nw;
-    if (G == 8) {
-        if (c <= 9) snr_rows<9, 8>(a, U, data, wl, nev, c, tid, tl);
-        else snr_rows<kSnrChunk, 8>(a, U, data, wl, nev, c, tid, tl);
-    } else if (G == 16) {
-        snr_rows<kSnrChunk, 16>(a, U, data, wl, nev, c, tid, tl);
-    } else if (G == 32) {
-        snr_rows<kSnrChunk, 32>(a, U, data, wl, nev, c, tid, tl);
+    if (c <= kSnrMaxChunk) {
+        if (G == 8) snr_rows<kSnrMaxChunk, 8>(a, U, data, q, wl, nev, c, tid, tl);
+        else if (G == 16) snr_rows<kSnrMaxChunk, 16>(a, U, data, q, wl, nev, c, tid, tl);
+        else if (G == 32) snr_rows<kSnrMaxChunk, 32>(a, U, data, q, wl, nev, c, tid, tl);
+        else snr_rows<kSnrMaxChunk, 64>(a, U, data, q, wl, nev, c, tid, tl);
     } else if (c <= kSnrChunk) {
-        snr_rows<kSnrChunk, 64>(a, U, data, wl, nev, c, tid, tl);
+        snr_rows<kSnrChunk, 64>(a, U, data, q, wl, nev, c, tid, tl);
     } else {
         // very wide rows (p > 64 * kSnrChunk): one wave per row, chunks from LDS
         const int g = lane;
@@ -1000,7 +1056,7 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
         for (int base = 0; base < nev; base += kConeWaves) {
             const int r = base + wave;
             const bool active = r < nev;
-            float* row = data + min(r, nev - 1) * p;
+            float* row = data + min(r, nev - 1) * q;
             double part = 0.0;
             for (int j = j0; j < j0 + cnt; ++j) part += (double)row[j];
             double incl = part;
@@ -1055,7 +1111,7 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
 // gets its own register allocation.  min 4 waves per SIMD: <= 128 VGPRs, two
 // workgroups per CU.
 template <int SMAX>
-__global__ __launch_bounds__(kConeBlock, 4) void cone_kernel(ConeArgs a)
+__global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(ConeArgs a)
 {
 #ifdef RT_STAMPS
     unsigned long long tl[kStampMarks] = {};
@@ -1077,7 +1133,8 @@ __global__ __launch_bounds__(kConeBlock, 4) void cone_kernel(ConeArgs a)
     const int p = U.p;
     const int L = U.levels;
     const bool tile = U.mode == kModeTile;
-    bool ok = uni(M.nrows[L]) * p <= kLdsDataFloats;
+    const int q = (int)row_stride((uint32_t)p);
+    bool ok = uni(M.nrows[L]) * p + 3 <= kLdsDataFloats;
     for (int l = 0; l <= L; ++l) ok = ok && uni(M.nrows[l]) <= lds_row_capacity((uint32_t)p, SMAX);
     if (!ok) {
         if (tid == 0 && a.error_flag) atomicOr(a.error_flag, 1);
@@ -1091,8 +1148,8 @@ __global__ __launch_bounds__(kConeBlock, 4) void cone_kernel(ConeArgs a)
     const bool use_table = entries <= kDescEntries;
     if (use_table) build_desc_table(M, desc, entries, p, L, tile, U.node_size, tid);
     RT_MARK(3);
-    float* const base = data + uni(F.al);
-    fill_land(F, base, (a.flags & kConeFillVec) != 0);
+    float* const base = data + uni(F.al);   // the filled level: dense rows, stride p
+    fill_land(F, base);
     lds_barrier();
     RT_MARK(4);
     // ---- merge levels, deepest first; a non-final pass stores its output
@@ -1104,26 +1161,28 @@ __global__ __launch_bounds__(kConeBlock, 4) void cone_kernel(ConeArgs a)
     const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(dst, (((uint32_t)U.m * (uint32_t)p + 3u) & ~3u) * 4u);
     const uint32_t o0 = (uint32_t)(U.node_start + U.s0) * (uint32_t)p * 4u;
     if (L > 0 && !(a.flags & kConeDiagNoMerge))
-        merge_levels<SMAX, merge_rows_per_wave(SMAX)>(M, base, desc, use_table, p, L, tile, U.node_size, tid, st_regs, rs,
-                                                      o0, (a.flags & kConeFuseLevels) != 0,
-                                                      a.flags);
+        merge_levels<SMAX, merge_rows_per_wave(SMAX)>(M, data, base, desc, use_table, p, q, L, tile, U.node_size,
+                                                      tid, st_regs, rs, o0, a.flags);
     RT_MARK(5);
     const int n0 = uni(M.nrows[0]);
+    // the output level: the filled level itself (L == 0: dense, at base) or
+    // the last merge level (stride q, at data)
+    float* const obuf = L == 0 ? base : data;
+    const int ostride = L == 0 ? p : q;
     if (st) {
         if (L == 0 || !st_regs) {
             // ---- store the output level from LDS (a single leaf row, or A/B)
-            const int E = n0 * p;
-            for (int e = tid; e < E; e += kConeBlock)
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(base[e]), rs, (int)(o0 + (uint32_t)e * 4u), 0, 0);
+            for (int r = 0; r < n0; ++r)
+                for (int j = tid; j < p; j += kConeBlock)
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(obuf[r * ostride + j]), rs,
+                                                          (int)(o0 + (uint32_t)(r * p + j) * 4u), 0, 0);
         }
-
     } else {
 #ifdef RT_STAMPS
-        if (!(a.flags & kConeDiagNoSnr)) snr_epilogue(a, U, base, wl, n0, tid, tl);
+        if (!(a.flags & kConeDiagNoSnr)) snr_epilogue(a, U, obuf, ostride, wl, n0, tid, tl);
 #else
-        if (!(a.flags & kConeDiagNoSnr)) snr_epilogue(a, U, base, wl, n0, tid, nullptr);
+        if (!(a.flags & kConeDiagNoSnr)) snr_epilogue(a, U, obuf, ostride, wl, n0, tid, nullptr);
 #endif
-
     }
 #ifdef RT_STAMPS
     if (tid == 0 && a.stamps) {
