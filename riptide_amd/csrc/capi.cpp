@@ -879,7 +879,7 @@ int rt_schedule_check(size_t size, double tsamp, size_t nw, double pmin, double 
                     const ConeNeed n = cone_need(it.node_size, it.s0, it.s1, it.levels, X.p);
                     if (n.max_rows > kMaxRows || n.max_floats > kLdsDataFloats || n.ranges > kMaxRanges)
                         throw std::runtime_error("schedule: tile exceeds the LDS budget");
-                } else if ((int)it.node_size * (int)row_stride(X.p) > kLdsDataFloats || it.node_size > (uint32_t)kMaxRows) {
+                } else if ((int)it.node_size * (int)X.p > kLdsDataFloats || it.node_size > (uint32_t)kMaxRows) {
                     throw std::runtime_error("schedule: whole node exceeds the LDS budget");
                 }
                 if (L.pass == last_pass[it.xform]) {

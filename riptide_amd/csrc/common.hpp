@@ -53,10 +53,6 @@ constexpr int kMaxRowsPerWave = kConeBlock >= 1024 ? 12 : 24;   // merge: staged
 // kLdsDataFloats and n <= kMaxRows.
 constexpr int kFillChunks = (kLdsDataFloats / 4 + kMaxRows + kConeBlock - 1) / kConeBlock;
 
-// LDS row stride of a level of p-bin rows: even (8-byte aligned bin pairs)
-// and > p (column p holds a copy of column 0).
-RT_HD inline uint32_t row_stride(uint32_t p) { return (p + 2u) & ~1u; }
-
 // Merge variant for rows of p phase bins: slots per row rounded up to an
 // instantiated width (1..5, 8, 16, 45); 0 if p is too wide for the LDS engine.
 RT_HD inline int merge_slots(uint32_t p)
@@ -81,7 +77,7 @@ RT_HD constexpr int merge_rows_per_wave(int smax)
 RT_HD inline int lds_row_capacity(uint32_t p, int smax)
 {
     if (!smax || p == 0) return 0;
-    int c = kLdsDataFloats / (int)row_stride(p);
+    int c = kLdsDataFloats / (int)p;
     const int stage = kConeWaves * merge_rows_per_wave(smax);
     if (stage < c) c = stage;
     return c < kMaxRows ? c : kMaxRows;
@@ -113,10 +109,13 @@ constexpr uint64_t kTimelineCap = 1u << 21;
 // cone kernel feature bits (ConeArgs::flags)
 enum : uint32_t {
     kConeStoreFromRegs = 1u,   // non-final passes store the output level straight from registers
+    kConeAddtid = 4u,          // level write-back by ds_write_addtid_b32 (SMAX <= 5)
     kConeDiagNoSnr = 1u << 30, // diagnostics only (wrong results): skip the S/N epilogue
     kConeDiagNoMerge = 1u << 29, // diagnostics only (wrong results): skip the merge levels
     kConeDiagNoWrite = 1u << 28, // diagnostics only (wrong results): skip the level write-back
     kConeDiagNoBarrier = 1u << 27, // diagnostics only (wrong results): no barriers between merge levels
+    kConeDiagNoLand = 1u << 26,  // diagnostics only (wrong results): fill loads issued but not landed in LDS
+    kConeDiagNoDesc = 1u << 25,  // diagnostics only (wrong results): no descriptor table
     kConeDefaultFeatures = 1u
 };
 enum : uint8_t { kSelLeaves = 0, kSelPing = 1, kSelPong = 2, kSelSnr = 3 };

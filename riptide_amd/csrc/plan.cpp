@@ -132,7 +132,7 @@ ConeNeed cone_need(uint32_t node_size, uint32_t s0, uint32_t s1, int levels, uin
         int rows = 0;
         for (const R& r : lv) rows += (int)(r.hi - r.lo + 1);
         need.max_rows = std::max(need.max_rows, rows);
-        need.max_floats = std::max(need.max_floats, rows * (int)row_stride(p));
+        need.max_floats = std::max(need.max_floats, rows * (int)p);
         need.ranges += (int)lv.size();
     };
     account(cur);
