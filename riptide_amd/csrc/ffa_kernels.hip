@@ -499,38 +499,46 @@ __device__ __forceinline__ void merge_level_dense(const UnitMeta& M, const float
                                                   int wave, int nr, float (&v)[RW][SMAX])
 {
     const int S = (p + 63) >> 6;
-    uint32_t d = 0;
+    // lane i unpacks the descriptor of the wave's i-th row into LDS float
+    // offsets (head row, tail row + shift) and the shift; the row loop takes
+    // them with v_readlane, so no per-row scalar unpacking or multiplies
+    int ho = 0, to = 0, sh = 0, car = 0;
     if (lane < nr) {
         const int r = wave + kConeWaves * lane;
+        uint32_t d;
         if (use_table) {
             d = desc[desc_offset(M, l) + r];
         } else {
-            int h, t, sh;
-            row_desc(M, tile, node_size, l, r, p, h, t, sh);
-            d = pack_desc(h, t, sh);
+            int h, t, s;
+            row_desc(M, tile, node_size, l, r, p, h, t, s);
+            d = pack_desc(h, t, s);
         }
+        const uint32_t tc = (d >> 10) & 1023u;
+        sh = (int)(d >> 20);
+        ho = (int)(d & 1023u) * p;
+        to = (tc == kCarried ? 0 : (int)tc * p) + sh;
+        car = tc == kCarried;
     }
     const lds_cptr l1 = (lds_cptr)src + lane;
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
-        const uint32_t dw = (uint32_t)__builtin_amdgcn_readlane((int)d, i);
-        const int h = (int)(dw & 1023u), sft = (int)(dw >> 20);
-        const uint32_t tc = (dw >> 10) & 1023u;
-        const int t = tc == kCarried ? 0 : (int)tc;
+        const int hoi = __builtin_amdgcn_readlane(ho, i);
+        const int toi = __builtin_amdgcn_readlane(to, i);
+        const int si = __builtin_amdgcn_readlane(sh, i);
         uint32_t keep = 0xFFFFFFFFu, neg0 = 0u;
         if (CARRIED) {
-            keep = tc == kCarried ? 0u : 0xFFFFFFFFu;
+            keep = __builtin_amdgcn_readlane(car, i) ? 0u : 0xFFFFFFFFu;
             neg0 = ~keep & 0x80000000u;
         }
-        const lds_cptr hrow = l1 + h * p;
-        lds_cptr ta = l1 + (t * p + sft);
+        const lds_cptr hrow = l1 + hoi;
+        lds_cptr ta = l1 + toi;
         lds_cptr tw = ta - p;
         asm("" : "+v"(ta), "+v"(tw));
-        const int thr = p - sft;
+        const int ls = lane + si;               // bin j = lane + 64k wraps when ls >= p - 64k
 #pragma unroll
         for (int k = 0; k < SMAX; ++k) {
             if (SMAX <= 5 || k < S) {
-                const lds_cptr tp = lane >= thr - 64 * k ? tw : ta;
+                const lds_cptr tp = ls >= p - 64 * k ? tw : ta;
                 float x = lds_ld(tp + 64 * k);
                 if (CARRIED) x = __uint_as_float((__float_as_uint(x) & keep) | neg0);
                 v[i][k] = __fadd_rn(lds_ld(hrow + 64 * k), x);
@@ -539,14 +547,6 @@ __device__ __forceinline__ void merge_level_dense(const UnitMeta& M, const float
     }
 }
 
-// All merge levels of one unit, deepest first.  SMAX >= ceil(p/64)
-// half-slots per row, RW rows per wave (lds_row_capacity(p, SMAX) guarantees
-// ceil(rows/8) <= RW at every level).  Each level's outputs are staged in
-// registers between two barriers (in-place update), then written back as
-// ds_write_b64 pairs (+ the single slot and the column-0 copy).  With `st`
-// set (a non-final pass), the output level goes from the staging registers
-// straight to global memory at byte offset st_o0 (rows of the tile are one
-// contiguous segment) instead of back into LDS.
 // Output level l == 0 of a non-final pass: straight from the staging
 // registers to global memory at byte offset st_o0 (the tile's rows are one
 // contiguous segment).
@@ -560,10 +560,14 @@ __device__ __forceinline__ void store_rows(const float (&v)[RW][SMAX], int p, in
         if (i < nr) {
             const uint32_t ob = st_o0 + (uint32_t)((wave + kConeWaves * i) * p + lane) * 4u;
 #pragma unroll
-            for (int k = 0; k < SMAX; ++k)
-                if ((SMAX <= 5 || k < S) && lane + 64 * k < p)
+            for (int k = 0; k < SMAX; ++k) {
+                // SMAX <= 5 kernels run rows of exactly SMAX slots: all but the
+                // last are full, so only the last needs a lane mask
+                const bool full = SMAX <= 5 ? k < SMAX - 1 : 64 * (k + 1) <= p;
+                if (full || ((SMAX <= 5 || k < S) && lane + 64 * k < p))
                     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs, (int)(ob + 256u * (uint32_t)k),
                                                           0, 0);
+            }
         }
     }
 }
@@ -650,8 +654,9 @@ __device__ __forceinline__ void write_rows(float* base, const float (&v)[RW][SMA
             float* orow = base + (wave + kConeWaves * i) * p + lane;
 #pragma unroll
             for (int k = 0; k < SMAX; ++k) {
-                if (64 * (k + 1) <= p) orow[64 * k] = v[i][k];            // full slot: no lane mask
-                else if ((SMAX <= 5 || k < S) && lane + 64 * k < p) orow[64 * k] = v[i][k];
+                // SMAX <= 5: all slots but the last are full (no lane mask)
+                const bool full = SMAX <= 5 ? k < SMAX - 1 : 64 * (k + 1) <= p;
+                if (full || ((SMAX <= 5 || k < S) && lane + 64 * k < p)) orow[64 * k] = v[i][k];
             }
         }
     }
@@ -1043,6 +1048,8 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
     const int L = U.levels;
     const bool tile = U.mode == kModeTile;
     bool ok = uni(M.nrows[L]) * p <= kLdsDataFloats;
+    // SMAX <= 5 variants assume rows of exactly SMAX slots (unmasked full slots)
+    ok = ok && (SMAX > 5 ? merge_slots((uint32_t)p) <= SMAX : merge_slots((uint32_t)p) == SMAX);
     for (int l = 0; l <= L; ++l) ok = ok && uni(M.nrows[l]) <= lds_row_capacity((uint32_t)p, SMAX);
     if (!ok) {
         if (tid == 0 && a.error_flag) atomicOr(a.error_flag, 1);
