@@ -271,11 +271,9 @@ __device__ __forceinline__ void setup_unit(const ConeArgs& a, int u, UnitMeta& M
         const int nb = uni(M.nrows[L]);
         const Range* lv = &M.ranges[(1 << L) - 1];
         for (int r = tid; r < nb; r += kConeBlock) {
-            int lo = 0, hi = (1 << L) - 1;
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (lv[mid].base <= r) lo = mid; else hi = mid - 1;
-            }
+            int lo = 0;
+            for (int step = (1 << L) >> 1; step > 0; step >>= 1)
+                if (lv[lo + step].base <= r) lo += step;
             const Range R = lv[lo];
             src_row[r] = R.start + R.lo + (r - R.base);
         }
@@ -402,12 +400,12 @@ __device__ __forceinline__ void row_desc(const UnitMeta& M, bool tile, int node_
                                          int& t, int& sh)
 {
     if (tile) {
+        // the last of the level's 2^l ranges starting at or before r: l
+        // halving steps (uniform trip count)
         const Range* lv = &M.ranges[(1 << l) - 1];
-        int lo = 0, hi = (1 << l) - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (lv[mid].base <= r) lo = mid; else hi = mid - 1;
-        }
+        int lo = 0;
+        for (int step = (1 << l) >> 1; step > 0; step >>= 1)
+            if (lv[lo + step].base <= r) lo += step;
         const Range R = lv[lo];
         const int u = R.lo + (r - R.base);
         const Range H = M.ranges[(2 << l) - 1 + 2 * lo];
@@ -541,7 +539,7 @@ __device__ __forceinline__ void merge_level_dense(const UnitMeta& M, const float
                 const lds_cptr tp = ls >= p - 64 * k ? tw : ta;
                 float x = lds_ld(tp + 64 * k);
                 if (CARRIED) x = __uint_as_float((__float_as_uint(x) & keep) | neg0);
-                v[i][k] = __fadd_rn(lds_ld(hrow + 64 * k), x);
+                v[i][k] = __fadd_rn(hrow[64 * k], x);
             }
         }
     }
