@@ -109,7 +109,6 @@ constexpr uint64_t kTimelineCap = 1u << 21;
 // cone kernel feature bits (ConeArgs::flags)
 enum : uint32_t {
     kConeStoreFromRegs = 1u,   // non-final passes store the output level straight from registers
-    kConeAddtid = 4u,          // level write-back by ds_write_addtid_b32 (SMAX <= 5)
     kConeDiagNoSnr = 1u << 30, // diagnostics only (wrong results): skip the S/N epilogue
     kConeDiagNoMerge = 1u << 29, // diagnostics only (wrong results): skip the merge levels
     kConeDiagNoWrite = 1u << 28, // diagnostics only (wrong results): skip the level write-back

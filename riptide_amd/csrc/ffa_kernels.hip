@@ -553,108 +553,50 @@ __device__ __forceinline__ void store_rows(const float (&v)[RW][SMAX], int p, in
                                            __amdgpu_buffer_rsrc_t rs, uint32_t st_o0)
 {
     const int S = (p + 63) >> 6;
+    const bool tail_ok = lane + 64 * (SMAX - 1) < p;
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
         if (i < nr) {
             const uint32_t ob = st_o0 + (uint32_t)((wave + kConeWaves * i) * p + lane) * 4u;
 #pragma unroll
             for (int k = 0; k < SMAX; ++k) {
-                // SMAX <= 5 kernels run rows of exactly SMAX slots: all but the
-                // last are full, so only the last needs a lane mask
-                const bool full = SMAX <= 5 ? k < SMAX - 1 : 64 * (k + 1) <= p;
-                if (full || ((SMAX <= 5 || k < S) && lane + 64 * k < p))
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs, (int)(ob + 256u * (uint32_t)k),
-                                                          0, 0);
+                if constexpr (SMAX <= 5) {
+                    // rows of exactly SMAX slots: the last slot's lanes past p
+                    // store out of the buffer's range, which drops them
+                    const uint32_t o = k < SMAX - 1 ? ob + 256u * (uint32_t)k
+                                                    : (tail_ok ? ob + 256u * (uint32_t)k : 0x80000000u);
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs, (int)o, 0, 0);
+                } else if (64 * (k + 1) <= p || (k < S && lane + 64 * k < p)) {
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs,
+                                                          (int)(ob + 256u * (uint32_t)k), 0, 0);
+                }
             }
         }
     }
 }
 
-// ds_write_addtid_b32: lane i stores to M0[15:0] + offset + 4i -- no address
-// VGPR and 2 LDS cycles per wave-instruction instead of ds_write_b32's 4
-// (tools/microbench/merge_loop.hip: -18 % per merge level).  One asm block
-// per row writes its F full slots (M0 = row base, the slot offsets
-// immediate; the SALU-writes-M0 -> add-TID hazard needs one wait state).
-// Issued by inline asm, so the writer waits (lgkmcnt) before the next
-// barrier itself.
-#define RT_ADDTID_HEAD "s_mov_b32 m0, %[m]\n\ts_nop 0\n\t"
-#define RT_ADDTID(i) "ds_write_addtid_b32 %[v" #i "] offset:%[o" #i "]\n\t"
-
-template <int HI, int F>
-__device__ __forceinline__ void addtid_slots(uint32_t m0, const float* v)
-{
-    if constexpr (F == 1) {
-        asm volatile(RT_ADDTID_HEAD RT_ADDTID(0) : : [m] "s"(m0), [v0] "v"(v[0]), [o0] "i"(HI) : "memory");
-    } else if constexpr (F == 2) {
-        asm volatile(RT_ADDTID_HEAD RT_ADDTID(0) RT_ADDTID(1)
-                     : : [m] "s"(m0), [v0] "v"(v[0]), [v1] "v"(v[1]), [o0] "i"(HI), [o1] "i"(HI + 256) : "memory");
-    } else if constexpr (F == 3) {
-        asm volatile(RT_ADDTID_HEAD RT_ADDTID(0) RT_ADDTID(1) RT_ADDTID(2)
-                     : : [m] "s"(m0), [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]), [o0] "i"(HI),
-                         [o1] "i"(HI + 256), [o2] "i"(HI + 512) : "memory");
-    } else if constexpr (F == 4) {
-        asm volatile(RT_ADDTID_HEAD RT_ADDTID(0) RT_ADDTID(1) RT_ADDTID(2) RT_ADDTID(3)
-                     : : [m] "s"(m0), [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]), [v3] "v"(v[3]),
-                         [o0] "i"(HI), [o1] "i"(HI + 256), [o2] "i"(HI + 512), [o3] "i"(HI + 768) : "memory");
-    } else if constexpr (F == 5) {
-        asm volatile(RT_ADDTID_HEAD RT_ADDTID(0) RT_ADDTID(1) RT_ADDTID(2) RT_ADDTID(3) RT_ADDTID(4)
-                     : : [m] "s"(m0), [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]), [v3] "v"(v[3]),
-                         [v4] "v"(v[4]), [o0] "i"(HI), [o1] "i"(HI + 256), [o2] "i"(HI + 512), [o3] "i"(HI + 768),
-                         [o4] "i"(HI + 1024) : "memory");
-    }
-}
-#undef RT_ADDTID_HEAD
-#undef RT_ADDTID
-
-// One row at LDS byte address rb (uniform) of a SMAX <= 5 level: its F full
-// slots (F = SMAX when p == 64 SMAX, else SMAX - 1; uniform per launch) by
-// add-TID, the partial slot by ds_write_b32.  Rows past 32 KiB take 0x8000
-// of their base into the immediates so M0 stays within 16 bits.
-template <int SMAX>
-__device__ __forceinline__ void write_row_addtid(uint32_t rb, float* orow, const float (&v)[SMAX], bool full, int lane,
-                                                 int p)
-{
-    if (full) {
-        if (rb < 0x8000u) addtid_slots<0, SMAX>(rb, v);
-        else addtid_slots<0x8000, SMAX>(rb - 0x8000u, v);
-    } else {
-        if constexpr (SMAX > 1) {
-            if (rb < 0x8000u) addtid_slots<0, SMAX - 1>(rb, v);
-            else addtid_slots<0x8000, SMAX - 1>(rb - 0x8000u, v);
-        }
-        if (lane + 64 * (SMAX - 1) < p) orow[lane + 64 * (SMAX - 1)] = v[SMAX - 1];
-    }
-}
-
 // Write-back of a level's staged rows into the dense LDS rows at `base`.
+// SMAX <= 5 kernels run rows of exactly SMAX slots: all but the last are
+// full; the last slot's lanes past p write to a dummy word in the LDS pad
+// (an address select instead of an exec-mask save/restore per row).
 template <int SMAX, int RW>
-__device__ __forceinline__ void write_rows(float* base, const float (&v)[RW][SMAX], int p, int lane, int wave, int nr,
-                                           bool addtid)
+__device__ __forceinline__ void write_rows(float* base, float* dummy, const float (&v)[RW][SMAX], int p, int lane,
+                                           int wave, int nr)
 {
     const int S = (p + 63) >> 6;
-    if (SMAX <= 5 && addtid) {
-        if constexpr (SMAX <= 5) {
-            const uint32_t b0 = (uint32_t)uni((int)(uint32_t)(size_t)(lds_cptr)base);
-            const bool full = p == 64 * SMAX;
-#pragma unroll
-            for (int i = 0; i < RW; ++i)
-                if (i < nr) {
-                    const int ro = (wave + kConeWaves * i) * p;
-                    write_row_addtid<SMAX>((uint32_t)uni((int)(b0 + (uint32_t)ro * 4u)), base + ro, v[i], full, lane, p);
-                }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
-        return;
-    }
+    const bool tail_ok = lane + 64 * (SMAX - 1) < p;
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
         if (i < nr) {
             float* orow = base + (wave + kConeWaves * i) * p + lane;
 #pragma unroll
             for (int k = 0; k < SMAX; ++k) {
-                // SMAX <= 5: all slots but the last are full (no lane mask)
-                const bool full = SMAX <= 5 ? k < SMAX - 1 : 64 * (k + 1) <= p;
-                if (full || ((SMAX <= 5 || k < S) && lane + 64 * k < p)) orow[64 * k] = v[i][k];
+                if constexpr (SMAX <= 5) {
+                    if (k < SMAX - 1) orow[64 * k] = v[i][k];
+                    else *(tail_ok ? orow + 64 * k : dummy) = v[i][k];
+                } else {
+                    if (64 * (k + 1) <= p || (k < S && lane + 64 * k < p)) orow[64 * k] = v[i][k];
+                }
             }
         }
     }
@@ -669,10 +611,9 @@ __device__ __forceinline__ void write_rows(float* base, const float (&v)[RW][SMA
 template <int SMAX, int RW>
 __device__ __forceinline__ void merge_levels(const UnitMeta& M, float* base, const uint32_t* desc, bool use_table,
                                              int p, int L, bool tile, int node_size, int tid, bool st,
-                                             __amdgpu_buffer_rsrc_t rs, uint32_t st_o0, uint32_t flags)
+                                             __amdgpu_buffer_rsrc_t rs, uint32_t st_o0, uint32_t flags, float* dummy)
 {
     const int lane = tid & 63, wave = tid >> 6;
-    const bool addtid = (flags & kConeAddtid) != 0;
     for (int l = L - 1; l >= 0; --l) {
         const int orows = uni(M.nrows[l]);
         const int nr = uni(orows > wave ? (orows - wave + kConeWaves - 1) / kConeWaves : 0);
@@ -687,7 +628,7 @@ __device__ __forceinline__ void merge_levels(const UnitMeta& M, float* base, con
             return;
         }
         if (!(flags & kConeDiagNoBarrier)) lds_barrier();
-        if (!(flags & kConeDiagNoWrite)) write_rows<SMAX, RW>(base, v, p, lane, wave, nr, addtid);
+        if (!(flags & kConeDiagNoWrite)) write_rows<SMAX, RW>(base, dummy, v, p, lane, wave, nr);
         if (!(flags & kConeDiagNoBarrier)) lds_barrier();
     }
 }
@@ -1076,7 +1017,7 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
     const uint32_t o0 = (uint32_t)(U.node_start + U.s0) * (uint32_t)p * 4u;
     if (L > 0 && !(a.flags & kConeDiagNoMerge))
         merge_levels<SMAX, merge_rows_per_wave(SMAX)>(M, base, desc, use_table, p, L, tile, U.node_size, tid, st_regs,
-                                                      rs, o0, a.flags);
+                                                      rs, o0, a.flags, data + kLdsDataFloats + 4 + (tid & 63));
     RT_MARK(5);
     const int n0 = uni(M.nrows[0]);
     // the output level, in place in the dense rows at base
