@@ -744,15 +744,27 @@ __device__ __forceinline__ float window_max(const float (&z)[CH + kSnrWin], cons
     return dm;
 }
 
-template <int CH, int W>
-struct WindowSwitch {
-    __device__ static __forceinline__ float run(int w, const float (&z)[CH + kSnrWin], const float (&cp)[CH])
-    {
-        if (w == W) return window_max<CH, W>(z, cp);
-        if constexpr (W < kSnrWin) return WindowSwitch<CH, W + 1>::run(w, z, cp);
-        return -INFINITY;
+// width dispatch: one switch (a jump, not a chain of scalar compares)
+template <int CH>
+__device__ __forceinline__ float window_dispatch(int w, const float (&z)[CH + kSnrWin], const float (&cp)[CH])
+{
+    static_assert(kSnrWin == 12, "cases below");
+    switch (w) {
+    case 1: return window_max<CH, 1>(z, cp);
+    case 2: return window_max<CH, 2>(z, cp);
+    case 3: return window_max<CH, 3>(z, cp);
+    case 4: return window_max<CH, 4>(z, cp);
+    case 5: return window_max<CH, 5>(z, cp);
+    case 6: return window_max<CH, 6>(z, cp);
+    case 7: return window_max<CH, 7>(z, cp);
+    case 8: return window_max<CH, 8>(z, cp);
+    case 9: return window_max<CH, 9>(z, cp);
+    case 10: return window_max<CH, 10>(z, cp);
+    case 11: return window_max<CH, 11>(z, cp);
+    case 12: return window_max<CH, 12>(z, cp);
+    default: return -INFINITY;
     }
-};
+}
 
 #ifdef RT_STAMPS
 #define RT_SNR_MARK(i)                                                           \
@@ -778,6 +790,7 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
     const int writer = kDpp ? G - 1 : 0;
     const uint32_t nw = a.num_widths;
     float* snr = a.snr + (uint64_t)U.trial * a.snr_stride + (U.snr_row + (uint64_t)U.s0) * (uint64_t)nw;
+    const __amdgpu_buffer_rsrc_t srs = buffer_rsrc(snr, (uint32_t)nev * nw * 4u);
     for (int base = 0; base < nev; base += rows_per_pass) {
         const int r = base + (tid / G);
         const bool active = r < nev;
@@ -814,10 +827,12 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
             cp[i] = (float)acc;
         }
         const float sum = __shfl((float)acc, owner, G);
-        if (active) {
+        {
+            // columns past the lane's chunk (and rows past nev) go to a dummy
+            // word in the LDS pad: an address select instead of exec masks
+            float* const dummy = data + kLdsDataFloats + 4 + lane;
 #pragma unroll
-            for (int i = 0; i < CH; ++i)
-                if (i < cnt) row[i] = cp[i];
+            for (int i = 0; i < CH; ++i) *((active && i < cnt) ? row + i : dummy) = cp[i];
         }
 #pragma unroll
         for (int i = 0; i < CH; ++i) cp[i] = i < cnt ? cp[i] : INFINITY;
@@ -825,13 +840,15 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
         lds_barrier();                        // prefix rows visible to all lanes
         RT_SNR_MARK(8);
         const float* crow = data + min(r, nev - 1) * q;
+        // one lane per row stores; the others store out of the buffer's
+        // range, which drops them (no exec-mask save/restore)
+        const uint32_t so = (active && g == writer) ? (uint32_t)r * nw * 4u : 0x80000000u;
         auto emit = [&](uint32_t iw, int w, float dmax) {
             dmax = seg_max_dpp<G>(dmax, lane);
-            if (active && g == writer) {
-                const float h = sqrtf((float)(p - w) / (float)(p * w));
-                const float b = (float)w / (float)(p - w) * h;
-                snr[(uint64_t)r * nw + iw] = ((h + b) * dmax - b * sum) / U.stdnoise;
-            }
+            const float h = sqrtf((float)(p - w) / (float)(p * w));
+            const float b = (float)w / (float)(p - w) * h;
+            const float v = ((h + b) * dmax - b * sum) / U.stdnoise;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srs, (int)(so + iw * 4u), 0, 0);
         };
         if constexpr (CH <= kSnrMaxChunk) {
             // widths <= kSnrWin from the register window c[j0 .. j0 + CH + kSnrWin)
@@ -851,7 +868,7 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
             RT_SNR_MARK(9);
             for (uint32_t iw = 0; iw < nw; ++iw) {
                 const int w = uni(wl[iw]);
-                if (w <= kSnrWin) emit(iw, w, WindowSwitch<CH, 1>::run(w, z, cp));
+                if (w <= kSnrWin) emit(iw, w, window_dispatch<CH>(w, z, cp));
             }
         }
         // wider widths: the window c[j0 + w ..] read from LDS per width
