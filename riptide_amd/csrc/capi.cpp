@@ -299,6 +299,7 @@ struct rt_plan {
     std::vector<DsRung> rungs;
     DsRung* d_rungs = nullptr;
     uint32_t ds_blocks = 0;
+    bool ds_fused = false;   // every rung fits the fused ladder's margin
     ~rt_plan()
     {
         if (d_rungs) (void)hipFree(d_rungs);
@@ -364,6 +365,9 @@ rt_plan* make_plan(size_t size, double tsamp, const uint64_t* widths, size_t nw,
             P->rungs.push_back(d);
         }
         P->ds_blocks = blocks;
+        P->ds_fused = !std::getenv("RIPTIDE_AMD_PER_RUNG_LADDER");
+        for (const DsRung& d : P->rungs)
+            if (!d.identity && std::ceil(d.f) + 2.0 > (double)kDsFusedMargin) P->ds_fused = false;
         ck(hipMalloc(&P->d_rungs, std::max<size_t>(1, P->rungs.size()) * sizeof(DsRung)), "hipMalloc");
         if (!P->rungs.empty())
             ck(hipMemcpy(P->d_rungs, P->rungs.data(), P->rungs.size() * sizeof(DsRung), hipMemcpyHostToDevice),
@@ -402,13 +406,19 @@ void run_periodogram(const rt_plan* P, const float* d_data, size_t batch, size_t
         r.b = g_prof.ev();
         ck(hipEventRecord(r.a, s), "hipEventRecord");
     }
-    ck(launch_downsample_ladder(d_data, P->pg.prm.size, data_stride, P->d_rungs, (uint32_t)P->rungs.size(),
-                                P->ds_blocks, leaves, P->pg.leaf_floats, (uint32_t)batch, s),
-       "downsample_ladder");
+    if (P->ds_fused)
+        ck(launch_downsample_fused(d_data, P->pg.prm.size, data_stride, P->d_rungs, (uint32_t)P->rungs.size(), leaves,
+                                   P->pg.leaf_floats, (uint32_t)batch, s),
+           "downsample_fused");
+    else
+        ck(launch_downsample_ladder(d_data, P->pg.prm.size, data_stride, P->d_rungs, (uint32_t)P->rungs.size(),
+                                    P->ds_blocks, leaves, P->pg.leaf_floats, (uint32_t)batch, s),
+           "downsample_ladder");
     if (g_prof.on) {
         ck(hipEventRecord(r.b, s), "hipEventRecord");
-        double bytes = 0;
-        for (const DsRung& d : P->rungs) bytes += 4.0 * (double)d.n + (d.identity ? 4.0 * d.n : 4.0 * P->pg.prm.size);
+        double bytes = P->ds_fused ? 4.0 * P->pg.prm.size : 0.0;   // fused: the series is read once
+        for (const DsRung& d : P->rungs)
+            bytes += 4.0 * (double)d.n + (P->ds_fused ? 0.0 : (d.identity ? 4.0 * d.n : 4.0 * P->pg.prm.size));
         r.alg = r.moved = bytes * batch;
         g_prof.rec[1].push_back(r);
     }

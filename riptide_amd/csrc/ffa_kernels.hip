@@ -75,6 +75,75 @@ __global__ __launch_bounds__(256) void downsample_ladder_kernel(
     out[k] = acc;
 }
 
+// Fused ladder: one block per input span (and trial) computes the outputs of
+// EVERY rung whose window starts in the span, so the series is read from HBM
+// once instead of once per rung (57 rungs at cfg2).  The span plus a margin
+// of kDsFusedMargin floats (>= ceil(f) + 2 for every fused rung) is staged in
+// LDS; each output is the same sequential window sum as the per-rung kernel.
+constexpr uint32_t kDsFusedSpan = kDsSpanFloats - kDsFusedMargin;
+
+// first output k of a rung whose window start floor(k f) is >= s
+__device__ __forceinline__ uint64_t ds_first_output(double f, uint64_t s)
+{
+    uint64_t k = (uint64_t)ceil((double)s / f);
+    while (k > 0 && (uint64_t)floor(__dmul_rn((double)(k - 1), f)) >= s) --k;
+    while ((uint64_t)floor(__dmul_rn((double)k, f)) < s) ++k;
+    return k;
+}
+
+__global__ __launch_bounds__(256) void downsample_fused_kernel(
+    const float* __restrict__ x, uint64_t n_in, uint64_t x_stride,
+    const DsRung* __restrict__ rungs, uint32_t num_rungs,
+    float* __restrict__ out, uint64_t out_stride)
+{
+    __shared__ float span[kDsSpanFloats];
+    const uint64_t s0 = (uint64_t)blockIdx.x * kDsFusedSpan;
+    const uint64_t s_end = min(s0 + (uint64_t)kDsFusedSpan, n_in);     // window starts owned by this block
+    const uint64_t l_end = min(s0 + (uint64_t)kDsSpanFloats, n_in);    // staged input
+    x += (uint64_t)blockIdx.y * x_stride;
+    out += (uint64_t)blockIdx.y * out_stride;
+    for (uint64_t i = s0 + threadIdx.x; i < l_end; i += 256) span[i - s0] = x[i];
+    __syncthreads();
+    const double last = (double)n_in - 1.0;
+    for (uint32_t ri = 0; ri < num_rungs; ++ri) {
+        const DsRung r = rungs[ri];
+        float* o = out + r.out_off;
+        if (r.identity) {
+            for (uint64_t k = s0 + threadIdx.x; k < min(s_end, r.n); k += 256) o[k] = span[k - s0];
+            continue;
+        }
+        const double f = r.f;
+        const uint64_t k_lo = ds_first_output(f, s0);
+        const uint64_t k_hi = min(s_end >= n_in ? r.n : ds_first_output(f, s_end), r.n);
+        for (uint64_t k = k_lo + threadIdx.x; k < k_hi; k += 256) {
+            const double start = __dmul_rn((double)k, f);
+            const double end = __dadd_rn(start, f);
+            const uint64_t imin = (uint64_t)floor(start);
+            double dmax = floor(end);
+            if (dmax > last) dmax = last;
+            const uint64_t imax = (uint64_t)dmax;
+            const float wmin = (float)__dsub_rn((double)(imin + 1), start);
+            const float wmax = (float)__dsub_rn(end, (double)imax);
+            const float* w = span + (imin - s0);
+            const uint32_t cnt = (uint32_t)(imax - imin);
+            float acc = __fmul_rn(wmin, w[0]);
+            for (uint32_t i = 1; i < cnt; ++i) acc = __fadd_rn(acc, w[i]);
+            acc = __fadd_rn(acc, __fmul_rn(wmax, w[cnt]));
+            o[k] = acc;
+        }
+    }
+}
+
+hipError_t launch_downsample_fused(const float* x, uint64_t n_in, uint64_t x_stride, const DsRung* d_rungs,
+                                   uint32_t num_rungs, float* out, uint64_t out_stride, uint32_t batch, hipStream_t s)
+{
+    if (!num_rungs || !batch || !n_in) return hipSuccess;
+    const uint64_t blocks = (n_in + kDsFusedSpan - 1) / kDsFusedSpan;
+    hipLaunchKernelGGL(downsample_fused_kernel, dim3((uint32_t)blocks, batch), dim3(256), 0, s, x, n_in, x_stride,
+                       d_rungs, num_rungs, out, out_stride);
+    return hipGetLastError();
+}
+
 hipError_t launch_downsample_ladder(const float* x, uint64_t n_in, uint64_t x_stride,
                                     const DsRung* d_rungs, uint32_t num_rungs, uint32_t total_blocks,
                                     float* out, uint64_t out_stride, uint32_t batch, hipStream_t s)

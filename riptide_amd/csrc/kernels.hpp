@@ -9,6 +9,7 @@
 namespace rt {
 
 constexpr uint32_t kDsSpanFloats = 8192;   // LDS input stage of the ladder kernel (32 KiB)
+constexpr uint32_t kDsFusedMargin = 1024;  // fused ladder: staged floats past the span (rungs with ceil(f) + 2 <= margin)
 
 struct DsRung {
     double f;
@@ -39,6 +40,9 @@ inline void ds_configure(DsRung& r)
 hipError_t launch_downsample_ladder(const float* x, uint64_t n_in, uint64_t x_stride,
                                     const DsRung* d_rungs, uint32_t num_rungs, uint32_t total_blocks,
                                     float* out, uint64_t out_stride, uint32_t batch, hipStream_t s);
+// all rungs of a periodogram from one read of the series (every rung: ceil(f) + 2 <= kDsFusedMargin)
+hipError_t launch_downsample_fused(const float* x, uint64_t n_in, uint64_t x_stride, const DsRung* d_rungs,
+                                   uint32_t num_rungs, float* out, uint64_t out_stride, uint32_t batch, hipStream_t s);
 // smax: merge_slots() bucket covering every transform of the launch
 hipError_t launch_cone(const ConeArgs& args, uint32_t grid, uint32_t smax, hipStream_t s);
 hipError_t launch_ffa_level(const float* in, float* out, const uint2* d_nodes, uint32_t num_nodes,

@@ -259,6 +259,27 @@ def test_batch_matches_single(rt):
         assert np.array_equal(dn[b].cpu().numpy(), ref)
 
 
+def test_fused_ladder_matches_per_rung(monkeypatch):
+    """The fused downsampling ladder (one read of the series for every rung)
+    produces exactly the per-rung kernel's leaves, hence identical S/N."""
+    import torch
+    from riptide_amd import engine
+    cases = [inputs.PGRAM_CASES[1], dict(n=1 << 22, tsamp=256e-6, pmin=0.1, pmax=10.0, bmin=240, bmax=260,
+                                         ducy_max=0.05)]
+    for case in cases:
+        x = torch.from_numpy(np.random.RandomState(7).normal(size=(2, case["n"])).astype(np.float32)).cuda()
+        outs = []
+        for per_rung in (False, True):
+            if per_rung:
+                monkeypatch.setenv("RIPTIDE_AMD_PER_RUNG_LADDER", "1")
+            else:
+                monkeypatch.delenv("RIPTIDE_AMD_PER_RUNG_LADDER", raising=False)
+            plan = engine.PeriodogramPlan.for_search(case["n"], case["tsamp"], case["pmin"], case["pmax"],
+                                                     case["bmin"], case["bmax"], ducy_max=case["ducy_max"])
+            outs.append(plan.run(x).cpu().numpy())
+        assert np.array_equal(outs[0], outs[1])
+
+
 # ---------------------------------------------------------------- full-size BASELINE configs
 @pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3", "cfg4"])
 def test_full_config(rt, golden_full, name):
