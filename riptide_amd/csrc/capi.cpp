@@ -123,7 +123,7 @@ uint64_t scratch_budget_floats()
         const double v = std::atof(e);
         if (v > 0) return (uint64_t)(v * 1e6);
     }
-    return 32ull << 20;
+    return 96ull << 20;   // 384 MiB per ping/pong buffer and trial: ~94 launches per cfg2 plan (sweep_schedule.py)
 }
 
 // ---- profiling of cone / downsample launches
@@ -344,7 +344,7 @@ rt_plan* make_plan(size_t size, double tsamp, const uint64_t* widths, size_t nw,
             X.stdnoise = s.stdnoise;
             xf.push_back(X);
         }
-        // scratch budget per ping/pong buffer and trial: 32 M floats (128 MiB)
+        // scratch budget per ping/pong buffer and trial (scratch_budget_floats)
         build_exec_plan(xf, true, (uint32_t)nw, scratch_budget_floats(), P->dp.ex);
         P->dp.upload();
         // downsample ladder over the rungs that feed at least one transform
