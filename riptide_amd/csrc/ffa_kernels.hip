@@ -158,25 +158,27 @@ hipError_t launch_downsample_ladder(const float* x, uint64_t n_in, uint64_t x_st
 // Cone kernel
 // ---------------------------------------------------------------------------
 // One workgroup (512 threads, 77 KiB of LDS: two workgroups per CU) per work
-// unit = one work item (UnitDesc) of one trial: `levels` merge levels of the FFA recursion
-// for the rows of one tile (or one whole node), held in LDS.  Phases:
+// unit = one work item (UnitDesc) of one trial: `levels` merge levels of the
+// FFA recursion for the rows of one tile (or one whole node), held in LDS.
+// Phases:
 //   1. setup: unit view, rows per level, range tree of tile units (the
 //      planner guarantees 2^l ranges at cone level l)
-//   2. LDS-DMA of the bottom level (dense rows, row stride p); while it is in
-//      flight, the row descriptors of every level are built into a table
+//   2. fill of the bottom level (dense rows, stride p): 16-byte buffer loads
+//      into registers; while they are in flight, the row descriptors of
+//      every level are built into a table; then landed in LDS
 //   3. merge levels, deepest first (transforms.hpp:13-27), one row per wave
 //      and one phase bin per lane:
 //          out[r][j] = H[h(r)][j] + T[t(r)][(j + shift(r)) mod p]
-//      The descriptor (head row, tail row, shift) is wave-uniform: lane i
-//      reads it for the wave's i-th row and the row loop takes it with
-//      v_readlane into SGPRs.  Bins j = lane + 64k use immediate offsets, so
-//      a 64-bin slot is one ds_read for H, one for T (consecutive lanes ->
-//      consecutive banks, conflict-free) and one ds_write.  A level's outputs
-//      are staged in registers between two barriers (in-place update).
-//   4. store the output rows (one contiguous segment), or the fused boxcar
-//      S/N epilogue (snr.hpp:37-65) when this is the transform's last pass.
+//      Lane i unpacks the descriptor of the wave's i-th row into LDS offsets;
+//      the row loop takes them with v_readlane.  Bins j = lane + 64k use
+//      immediate offsets, so a 64-bin slot is one ds_read for H, one for T
+//      (consecutive lanes -> consecutive banks) and one ds_write.  A level's
+//      outputs are staged in registers between two barriers (in place).
+//   4. a non-final pass stores its last level straight from the registers;
+//      a final pass runs the fused boxcar S/N epilogue (snr.hpp:37-65) on it.
 // The other workgroup on the CU overlaps its latency-bound phases (setup,
-// DMA wait, epilogue) with this one's LDS work.
+// fill wait) with this one's LDS and VALU work; the kernel as a whole is
+// bound by the CU's LDS, VALU and scalar issue.
 struct Range {          // rows [lo, hi] of one node of the split tree
     int size;           // rows of the node
     int lo, hi;         // node-local rows
@@ -186,7 +188,7 @@ struct Range {          // rows [lo, hi] of one node of the split tree
 
 
 // LDS-only workgroup barrier: orders LDS accesses without waiting for the
-// global loads (the next unit's prefetch) that are still in flight.
+// global loads or stores that are still in flight.
 __device__ __forceinline__ void lds_barrier()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
