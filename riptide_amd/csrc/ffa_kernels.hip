@@ -848,7 +848,7 @@ __device__ __forceinline__ float window_dispatch(int w, const float (&z)[CH + kS
 
 template <int CH, int G>
 __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, float* data, int q, const int* wl,
-                                         int nev, int c, int tid, unsigned long long* tl)
+                                         int nev, int c, int tid, const float* whb, unsigned long long* tl)
 {
     constexpr bool kDpp = true;
     const int lane = tid & 63;
@@ -915,10 +915,12 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
         // range, which drops them (no exec-mask save/restore)
         const uint32_t so = (active && g == writer) ? (uint32_t)r * nw * 4u : 0x80000000u;
         auto emit = [&](uint32_t iw, int w, float dmax) {
+            (void)w;
             dmax = seg_max_dpp<G>(dmax, lane);
-            const float h = sqrtf((float)(p - w) / (float)(p * w));
-            const float b = (float)w / (float)(p - w) * h;
-            const float v = ((h + b) * dmax - b * sum) / U.stdnoise;
+            // h + b and b of this width (per unit, in LDS: uniform reads)
+            const float hpb = __int_as_float(uni(__float_as_int(whb[2 * iw])));
+            const float b = __int_as_float(uni(__float_as_int(whb[2 * iw + 1])));
+            const float v = (hpb * dmax - b * sum) / U.stdnoise;
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srs, (int)(so + iw * 4u), 0, 0);
         };
         if constexpr (CH <= kSnrMaxChunk) {
@@ -967,12 +969,21 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
 }
 
 __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& U, float* data, int q, const int* wl,
-                                             int nrows, int tid, unsigned long long* tl)
+                                             int nrows, int tid, float* whb, unsigned long long* tl)
 {
     const int lane = tid & 63, wave = tid >> 6;
     const int p = U.p;
     const int nev = (int)min((int64_t)nrows, (int64_t)U.rows_eval - (int64_t)U.s0);
     if (nev <= 0) return;
+    // per-width constants of the S/N formula (snr.hpp:37-65), once per unit;
+    // visible to every wave after the first barrier of the row passes
+    if (tid < (int)a.num_widths) {
+        const int w = wl[tid];
+        const float h = sqrtf((float)(p - w) / (float)(p * w));
+        const float b = (float)w / (float)(p - w) * h;
+        whb[2 * tid] = h + b;
+        whb[2 * tid + 1] = b;
+    }
     // G lanes per row: the smallest power of two >= 8 whose chunks fit
     // kSnrMaxChunk columns (17 at G = 64); chunk lengths odd
     int G = 8;
@@ -982,12 +993,12 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
     const uint32_t nw = a.num_widths;
     float* snr = a.snr + (uint64_t)U.trial * a.snr_stride + (U.snr_row + (uint64_t)U.s0) * (uint64_t)nw;
     if (c <= kSnrMaxChunk) {
-        if (G == 8) snr_rows<kSnrMaxChunk, 8>(a, U, data, q, wl, nev, c, tid, tl);
-        else if (G == 16) snr_rows<kSnrMaxChunk, 16>(a, U, data, q, wl, nev, c, tid, tl);
-        else if (G == 32) snr_rows<kSnrMaxChunk, 32>(a, U, data, q, wl, nev, c, tid, tl);
-        else snr_rows<kSnrMaxChunk, 64>(a, U, data, q, wl, nev, c, tid, tl);
+        if (G == 8) snr_rows<kSnrMaxChunk, 8>(a, U, data, q, wl, nev, c, tid, whb, tl);
+        else if (G == 16) snr_rows<kSnrMaxChunk, 16>(a, U, data, q, wl, nev, c, tid, whb, tl);
+        else if (G == 32) snr_rows<kSnrMaxChunk, 32>(a, U, data, q, wl, nev, c, tid, whb, tl);
+        else snr_rows<kSnrMaxChunk, 64>(a, U, data, q, wl, nev, c, tid, whb, tl);
     } else if (c <= kSnrChunk) {
-        snr_rows<kSnrChunk, 64>(a, U, data, q, wl, nev, c, tid, tl);
+        snr_rows<kSnrChunk, 64>(a, U, data, q, wl, nev, c, tid, whb, tl);
     } else {
         // very wide rows (p > 64 * kSnrChunk): one wave per row, chunks from LDS
         const int g = lane;
@@ -1063,6 +1074,7 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
     __shared__ uint32_t desc[kDescEntries];
     __shared__ int src_row[kMaxRows];
     __shared__ int wl[kMaxWidths];   // boxcar widths: LDS reads never wait on the S/N stores in flight
+    __shared__ float whb[2 * kMaxWidths];   // S/N: h + b and b per width
 
     const int tid = threadIdx.x;
     const int u = (int)blockIdx.x;
@@ -1121,9 +1133,9 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
         }
     } else {
 #ifdef RT_STAMPS
-        if (!(a.flags & kConeDiagNoSnr)) snr_epilogue(a, U, obuf, ostride, wl, n0, tid, tl);
+        if (!(a.flags & kConeDiagNoSnr)) snr_epilogue(a, U, obuf, ostride, wl, n0, tid, whb, tl);
 #else
-        if (!(a.flags & kConeDiagNoSnr)) snr_epilogue(a, U, obuf, ostride, wl, n0, tid, nullptr);
+        if (!(a.flags & kConeDiagNoSnr)) snr_epilogue(a, U, obuf, ostride, wl, n0, tid, whb, nullptr);
 #endif
     }
 #ifdef RT_STAMPS
