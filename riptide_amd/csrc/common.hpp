@@ -28,26 +28,32 @@
 namespace rt {
 
 // ---- cone kernel geometry (gfx950: 160 KiB LDS per CU).  512-thread
-// workgroups with ~77 KiB of LDS each, two per CU; the level buffer holds
-// dense rows (stride p).
+// workgroups; RT_CONE_WGS = 2: ~77 KiB of LDS each, two per CU; RT_CONE_WGS =
+// 1: one ~155 KiB workgroup per CU (twice the rows per unit, so fewer HBM
+// passes, 256 VGPRs per lane).  The level buffer holds dense rows (stride p).
 #ifndef RT_CONE_BLOCK
 #define RT_CONE_BLOCK 512
 #endif
+#ifndef RT_CONE_WGS
+#define RT_CONE_WGS 2
+#endif
+constexpr int kConeWgsPerCu = RT_CONE_WGS;
+static_assert(kConeWgsPerCu >= 1 && kConeWgsPerCu <= 3, "RT_CONE_WGS is 1, 2 or 3");
 constexpr int kConeBlock = RT_CONE_BLOCK;   // 8 waves; two workgroups per CU (RT_CONE_BLOCK=1024: 16 waves, 64 VGPRs, measured slower)
 constexpr int kConeWaves = kConeBlock / 64;
-constexpr int kConeWavesPerSimd = 2 * kConeWaves / 4;
-constexpr int kLdsDataFloats = 17408;       // 68 KiB level buffer
+constexpr int kConeWavesPerSimd = kConeWgsPerCu * kConeWaves / 4;
+constexpr int kLdsDataFloats = kConeWgsPerCu == 1 ? 36864 : (kConeWgsPerCu == 2 ? 17408 : 11264);   // 144 | 68 | 44 KiB level buffer
 constexpr int kLdsPadFloats = 128;          // slack read (never used) by the unused slots of the last row
 constexpr int kMaxRows = 512;               // rows per level (source-row table, descriptors)
-constexpr int kDescEntries = 1024;          // row-descriptor table (all levels of a unit)
+constexpr int kDescEntries = kConeWgsPerCu == 1 ? 2048 : (kConeWgsPerCu == 2 ? 1024 : 768);   // row-descriptor table (all levels of a unit)
 constexpr int kMaxTileLevels = 6;           // L for tile items
 constexpr int kMaxLevels = 11;              // merge levels of any unit (whole units: ceil(log2(kMaxRows)))
 constexpr int kMaxRanges = (1 << (kMaxTileLevels + 1)) - 1;
 constexpr int kMaxWidths = 32;              // boxcar widths handled by the fused S/N epilogue
 constexpr int kSnrChunk = 17;               // S/N epilogue: columns per lane held in registers
-constexpr int kStageRegs = kConeBlock >= 1024 ? 25 : 45;   // merge: staged values per lane (rows x slots)
+constexpr int kStageRegs = kConeBlock >= 1024 || kConeWgsPerCu == 3 ? 25 : (kConeWgsPerCu == 1 ? 96 : 45);   // merge: staged values per lane (rows x slots)
 constexpr int kMaxSlots = 45;               // merge: 64-bin slots per row (p <= 2880)
-constexpr int kMaxRowsPerWave = kConeBlock >= 1024 ? 12 : 24;   // merge: staged rows per wave
+constexpr int kMaxRowsPerWave = kConeBlock >= 1024 || kConeWgsPerCu == 3 ? 12 : (kConeWgsPerCu == 1 ? 48 : 24);   // merge: staged rows per wave
 // float4 chunks per thread of the fill: a level of n rows spans at most
 // n*p/4 + n aligned chunks (one extra per row for misalignment), n*p <=
 // kLdsDataFloats and n <= kMaxRows.

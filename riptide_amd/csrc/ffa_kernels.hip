@@ -717,7 +717,7 @@ __device__ __forceinline__ void merge_levels(const UnitMeta& M, float* base, con
 constexpr int kSnrWin = 12;
 // S/N chunk columns per lane held in registers (and the window path), by the
 // register budget of the block size
-constexpr int kSnrMaxChunk = kConeBlock >= 1024 ? 9 : 17;
+constexpr int kSnrMaxChunk = kConeBlock >= 1024 || kConeWgsPerCu == 3 ? 9 : 17;
 
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v)
