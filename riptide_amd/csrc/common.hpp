@@ -60,31 +60,47 @@ constexpr int kMaxRowsPerWave = kConeBlock >= 1024 || kConeWgsPerCu == 3 ? 12 : 
 constexpr int kFillChunks = (kLdsDataFloats / 4 + kMaxRows + kConeBlock - 1) / kConeBlock;
 
 // Merge variant for rows of p phase bins: slots per row rounded up to an
-// instantiated width (1..5, 8, 16, 45); 0 if p is too wide for the LDS engine.
+// instantiated width (1..5, 8, 16, 45), or kPack2 for p <= 32 (two rows per
+// wave instruction, lanes 0-31 and 32-63); 0 if p is too wide for the LDS
+// engine.  The value is the cone kernel's template argument and launch bucket.
+#ifndef RT_PACK_SMALL_ROWS
+#define RT_PACK_SMALL_ROWS 0
+#endif
+constexpr int kPack2 = 64;
 RT_HD inline int merge_slots(uint32_t p)
 {
+    if (RT_PACK_SMALL_ROWS && p <= 32) return kPack2;
+    if (p == 0) return 1;
     const int s = (int)((p + 63) / 64);
-    if (s <= 5) return s < 1 ? 1 : s;
+    if (s <= 5) return s;
     if (s <= 8) return 8;
     if (s <= 16) return 16;
     if (s <= kMaxSlots) return kMaxSlots;
     return 0;
 }
 
-// Rows per wave the merge stages for a slot width (register budget).
+// 64-lane slots per register row of a merge variant, and rows per slot
+RT_HD constexpr int slot_count(int smax) { return smax == kPack2 ? 1 : smax; }
+RT_HD constexpr int row_pack(int smax) { return smax == kPack2 ? 2 : 1; }
+
+// Register rows per wave the merge stages for a variant (register budget);
+// each register row holds row_pack(smax) output rows.
 RT_HD constexpr int merge_rows_per_wave(int smax)
 {
-    return kStageRegs / smax < 1 ? 1 : (kStageRegs / smax < kMaxRowsPerWave ? kStageRegs / smax : kMaxRowsPerWave);
+    return kStageRegs / slot_count(smax) < 1
+               ? 1
+               : (kStageRegs / slot_count(smax) < kMaxRowsPerWave ? kStageRegs / slot_count(smax) : kMaxRowsPerWave);
 }
 
 // Row capacity of one cone work unit for p phase bins run by the kernel
-// variant of slot width smax (>= merge_slots(p)): the level buffer, and the
-// register staging of a level (merge_rows_per_wave(smax) rows per wave).
+// variant smax (merge_slots(p), or a wider slot width): the level buffer, and
+// the register staging of a level (merge_rows_per_wave(smax) register rows
+// of row_pack(smax) rows per wave).
 RT_HD inline int lds_row_capacity(uint32_t p, int smax)
 {
     if (!smax || p == 0) return 0;
     int c = kLdsDataFloats / (int)p;
-    const int stage = kConeWaves * merge_rows_per_wave(smax);
+    const int stage = kConeWaves * merge_rows_per_wave(smax) * row_pack(smax);
     if (stage < c) c = stage;
     return c < kMaxRows ? c : kMaxRows;
 }

@@ -616,6 +616,58 @@ __device__ __forceinline__ void merge_level_dense(const UnitMeta& M, const float
     }
 }
 
+// kPack2 variant (p <= 32): register row i of a wave holds two output rows,
+// the wave's row 2i in lanes 0-31 and row 2i + 1 in lanes 32-63 (bin j =
+// lane & 31), so a wave instruction does the work of two rows instead of
+// leaving 32-48 of its 64 lanes idle.  Each half takes its row's offsets with
+// its own v_readlane and a select; otherwise as merge_level_dense (same
+// additions, same -0.0 carry masking).
+template <int RW, bool CARRIED>
+__device__ __forceinline__ void merge_level_packed(const UnitMeta& M, const float* src, const uint32_t* desc,
+                                                   bool use_table, int p, int l, bool tile, int node_size, int lane,
+                                                   int wave, int nr, float (&v)[RW][1])
+{
+    int ho = 0, to = 0, sh = 0, car = 0;
+    if (lane < nr) {
+        const int r = wave + kConeWaves * lane;
+        uint32_t d;
+        if (use_table) {
+            d = desc[desc_offset(M, l) + r];
+        } else {
+            int h, t, s;
+            row_desc(M, tile, node_size, l, r, p, h, t, s);
+            d = pack_desc(h, t, s);
+        }
+        const uint32_t tc = (d >> 10) & 1023u;
+        sh = (int)(d >> 20);
+        ho = (int)(d & 1023u) * p;
+        to = (tc == kCarried ? 0 : (int)tc * p) + sh;
+        car = tc == kCarried;
+    }
+    const bool hi = lane >= 32;
+    const int j = lane & 31;
+    const lds_cptr l1 = (lds_cptr)src + j;
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+        const int hoi = hi ? __builtin_amdgcn_readlane(ho, 2 * i + 1) : __builtin_amdgcn_readlane(ho, 2 * i);
+        const int toi = hi ? __builtin_amdgcn_readlane(to, 2 * i + 1) : __builtin_amdgcn_readlane(to, 2 * i);
+        const int si = hi ? __builtin_amdgcn_readlane(sh, 2 * i + 1) : __builtin_amdgcn_readlane(sh, 2 * i);
+        uint32_t keep = 0xFFFFFFFFu, neg0 = 0u;
+        if (CARRIED) {
+            const int ci = hi ? __builtin_amdgcn_readlane(car, 2 * i + 1) : __builtin_amdgcn_readlane(car, 2 * i);
+            keep = ci ? 0u : 0xFFFFFFFFu;
+            neg0 = ~keep & 0x80000000u;
+        }
+        const lds_cptr hrow = l1 + hoi;
+        lds_cptr ta = l1 + toi;
+        lds_cptr tw = ta - p;
+        asm("" : "+v"(ta), "+v"(tw));
+        float x = lds_ld(j + si >= p ? tw : ta);
+        if (CARRIED) x = __uint_as_float((__float_as_uint(x) & keep) | neg0);
+        v[i][0] = __fadd_rn(hrow[0], x);
+    }
+}
+
 // Output level l == 0 of a non-final pass: straight from the staging
 // registers to global memory at byte offset st_o0 (the tile's rows are one
 // contiguous segment).
@@ -673,6 +725,39 @@ __device__ __forceinline__ void write_rows(float* base, float* dummy, const floa
     }
 }
 
+// kPack2 store / write-back: lane half h of register row i is the wave's row
+// 2i + h; halves past nr and bins past p store out of the buffer's range
+// (dropped) or to the LDS dummy word.
+template <int RW>
+__device__ __forceinline__ void store_rows_packed(const float (&v)[RW][1], int p, int lane, int wave, int nr,
+                                                  __amdgpu_buffer_rsrc_t rs, uint32_t st_o0)
+{
+    const int hi = lane >> 5, j = lane & 31;
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+        if (2 * i < nr) {
+            const int k = 2 * i + hi;
+            const uint32_t o = (k < nr && j < p) ? st_o0 + (uint32_t)((wave + kConeWaves * k) * p + j) * 4u
+                                                 : 0x80000000u;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][0]), rs, (int)o, 0, 0);
+        }
+    }
+}
+
+template <int RW>
+__device__ __forceinline__ void write_rows_packed(float* base, float* dummy, const float (&v)[RW][1], int p, int lane,
+                                                  int wave, int nr)
+{
+    const int hi = lane >> 5, j = lane & 31;
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+        if (2 * i < nr) {
+            const int k = 2 * i + hi;
+            *((k < nr && j < p) ? base + (wave + kConeWaves * k) * p + j : dummy) = v[i][0];
+        }
+    }
+}
+
 // All merge levels of one unit, deepest first, in place in the dense rows
 // at `base`.  SMAX >= ceil(p/64) slots per row, RW rows per wave
 // (lds_row_capacity(p, SMAX) guarantees ceil(rows/8) <= RW at every level).
@@ -688,18 +773,31 @@ __device__ __forceinline__ void merge_levels(const UnitMeta& M, float* base, con
     for (int l = L - 1; l >= 0; --l) {
         const int orows = uni(M.nrows[l]);
         const int nr = uni(orows > wave ? (orows - wave + kConeWaves - 1) / kConeWaves : 0);
-        float v[RW][SMAX];
+        constexpr int S = slot_count(SMAX);
+        float v[RW][S];
         // size-1 nodes exist at depth l only in whole units with node_size >> l < 2
-        if (!tile && (node_size >> l) < 2)
-            merge_level_dense<SMAX, RW, true>(M, base, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
-        else
-            merge_level_dense<SMAX, RW, false>(M, base, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
+        const bool carried = !tile && (node_size >> l) < 2;
+        if constexpr (SMAX == kPack2) {
+            if (carried)
+                merge_level_packed<RW, true>(M, base, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
+            else
+                merge_level_packed<RW, false>(M, base, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
+        } else {
+            if (carried)
+                merge_level_dense<S, RW, true>(M, base, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
+            else
+                merge_level_dense<S, RW, false>(M, base, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
+        }
         if (l == 0 && st) {
-            store_rows<SMAX, RW>(v, p, lane, wave, nr, rs, st_o0);
+            if constexpr (SMAX == kPack2) store_rows_packed<RW>(v, p, lane, wave, nr, rs, st_o0);
+            else store_rows<S, RW>(v, p, lane, wave, nr, rs, st_o0);
             return;
         }
         if (!(flags & kConeDiagNoBarrier)) lds_barrier();
-        if (!(flags & kConeDiagNoWrite)) write_rows<SMAX, RW>(base, dummy, v, p, lane, wave, nr);
+        if (!(flags & kConeDiagNoWrite)) {
+            if constexpr (SMAX == kPack2) write_rows_packed<RW>(base, dummy, v, p, lane, wave, nr);
+            else write_rows<S, RW>(base, dummy, v, p, lane, wave, nr);
+        }
         if (!(flags & kConeDiagNoBarrier)) lds_barrier();
     }
 }
@@ -993,7 +1091,10 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
     const uint32_t nw = a.num_widths;
     float* snr = a.snr + (uint64_t)U.trial * a.snr_stride + (U.snr_row + (uint64_t)U.s0) * (uint64_t)nw;
     if (c <= kSnrMaxChunk) {
-        if (G == 8) snr_rows<kSnrMaxChunk, 8>(a, U, data, q, wl, nev, c, tid, whb, tl);
+        // short rows (p <= 40 / 72): register chunks sized to the row, not 17
+        if (G == 8 && c <= 5) snr_rows<5, 8>(a, U, data, q, wl, nev, c, tid, whb, tl);
+        else if (G == 8 && c <= 9) snr_rows<9, 8>(a, U, data, q, wl, nev, c, tid, whb, tl);
+        else if (G == 8) snr_rows<kSnrMaxChunk, 8>(a, U, data, q, wl, nev, c, tid, whb, tl);
         else if (G == 16) snr_rows<kSnrMaxChunk, 16>(a, U, data, q, wl, nev, c, tid, whb, tl);
         else if (G == 32) snr_rows<kSnrMaxChunk, 32>(a, U, data, q, wl, nev, c, tid, whb, tl);
         else snr_rows<kSnrMaxChunk, 64>(a, U, data, q, wl, nev, c, tid, whb, tl);
@@ -1088,7 +1189,9 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
     const bool tile = U.mode == kModeTile;
     bool ok = uni(M.nrows[L]) * p <= kLdsDataFloats;
     // SMAX <= 5 variants assume rows of exactly SMAX slots (unmasked full slots)
-    ok = ok && (SMAX > 5 ? merge_slots((uint32_t)p) <= SMAX : merge_slots((uint32_t)p) == SMAX);
+    // (kPack2 runs exactly the p <= 32 rows)
+    ok = ok && ((SMAX <= 5 || SMAX == kPack2) ? merge_slots((uint32_t)p) == SMAX
+                                              : (merge_slots((uint32_t)p) <= SMAX && merge_slots((uint32_t)p) != kPack2));
     for (int l = 0; l <= L; ++l) ok = ok && uni(M.nrows[l]) <= lds_row_capacity((uint32_t)p, SMAX);
     if (!ok) {
         if (tid == 0 && a.error_flag) atomicOr(a.error_flag, 1);
@@ -1167,6 +1270,7 @@ hipError_t launch_cone(const ConeArgs& args, uint32_t grid, uint32_t smax, hipSt
     case 8: hipLaunchKernelGGL(cone_kernel<8>, g, b, 0, s, args); break;
     case 16: hipLaunchKernelGGL(cone_kernel<16>, g, b, 0, s, args); break;
     case kMaxSlots: hipLaunchKernelGGL(cone_kernel<kMaxSlots>, g, b, 0, s, args); break;
+    case kPack2: hipLaunchKernelGGL(cone_kernel<kPack2>, g, b, 0, s, args); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -2,7 +2,7 @@
 """A/B of cone-kernel feature bits (RIPTIDE_AMD_CONE_FLAGS, read per launch
 batch) on the cfg2 workload: ms per trial of the periodogram for each value.
 
-usage (GPU box): python tools/ab_flags.py 3,2,1,0
+usage (GPU box): python tools/ab_flags.py 3,2,1,0 [cfg1|cfg2|cfg3|cfg4]
 """
 import json
 import os
@@ -11,15 +11,19 @@ import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
 def main():
     import torch
     from riptide_amd import engine
-    n = 1 << 23
+    from bench_configs import CONFIGS
     flags = sys.argv[1].split(",") if len(sys.argv) > 1 else ["3", "0"]
+    c = {k["name"]: k for k in CONFIGS}[sys.argv[2] if len(sys.argv) > 2 else "cfg2"]
+    n = c["n"]
     B = 8
-    plan = engine.PeriodogramPlan.for_search(n, 256e-6, 0.1, 10.0, 240, 260, ducy_max=0.05)
+    plan = engine.PeriodogramPlan.for_search(n, c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"],
+                                             ducy_max=c["ducy_max"])
     x = torch.randn((B, n), device="cuda", dtype=torch.float32)
     out = torch.empty((B, plan.length, plan.num_widths), device="cuda", dtype=torch.float32)
     ws = torch.empty(plan.workspace_bytes(B), dtype=torch.uint8, device="cuda")
