@@ -952,8 +952,8 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
     const int lane = tid & 63;
     const int p = U.p;
     const int g = lane & (G - 1);
-    const int j0 = min(g * c, p);
-    const int cnt = min(j0 + c, p) - j0;          // columns of this lane (may be 0)
+    int j0 = min(g * c, p);
+    int cnt = min(j0 + c, p) - j0;                // columns of this lane (may be 0)
     const int owner = (p - 1) / c;
     const int rows_per_pass = kConeBlock / G;
     const int writer = kDpp ? G - 1 : 0;
@@ -961,6 +961,10 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
     float* snr = a.snr + (uint64_t)U.trial * a.snr_stride + (U.snr_row + (uint64_t)U.s0) * (uint64_t)nw;
     const __amdgpu_buffer_rsrc_t srs = buffer_rsrc(snr, (uint32_t)nev * nw * 4u);
     for (int base = 0; base < nev; base += rows_per_pass) {
+        // opaque per row pass: the column masks (i < cnt, j0 + k >= p) are
+        // recomputed by one v_cmp each instead of being hoisted out of the
+        // loop into SGPR pairs that spill (two v_readlane per use)
+        asm volatile("" : "+v"(j0), "+v"(cnt));
         const int r = base + (tid / G);
         const bool active = r < nev;
         float* row = data + min(r, nev - 1) * q + j0;
