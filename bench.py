@@ -78,6 +78,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
+    # transform-group scratch per ping/pong buffer and trial (capi.cpp
+    # scratch_budget_floats): 384 M floats = 26 instead of 94 cone launches per
+    # step, ~1 % faster (tools/ab_sched.py); 49 GB of the 288 GB HBM at 16 trials
+    os.environ.setdefault("RIPTIDE_AMD_SCRATCH_MFLOATS", "384")
     import torch
     import torch.distributed as dist
     from riptide_amd import engine
@@ -153,6 +157,7 @@ def main():
                 "trial_periods": plan.length,
                 "ffa_transforms": stats["transforms"],
                 "cone_launches_per_step": stats["launches"],
+                "scratch_mfloats_per_buffer_trial": float(os.environ["RIPTIDE_AMD_SCRATCH_MFLOATS"]),
                 "parallelism": f"dm-trials x{world} (independent, weak scaling)",
             },
             "roofline": {
