@@ -1070,6 +1070,23 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
     }
 }
 
+// Phase-bin range [lo, hi] a cone kernel variant runs, and the S/N lane-group
+// size G of a row of p bins: the epilogue instantiates only the row shapes its
+// variant can meet (smaller kernels; the rest is compiled out).
+constexpr int snr_group(int p)
+{
+    int G = 8;
+    while (G < 64 && ((((p + G - 1) / G) | 1) > kSnrMaxChunk)) G <<= 1;
+    return G;
+}
+constexpr int variant_pmin(int smax) { return smax == kPack2 ? 1 : (smax <= 5 ? 64 * (smax - 1) + 1 : (smax == 8 ? 321 : (smax == 16 ? 513 : 1025))); }
+constexpr int variant_pmax(int smax) { return smax == kPack2 ? 32 : (smax <= 5 ? 64 * smax : (smax == 8 ? 512 : (smax == 16 ? 1024 : 64 * kMaxSlots))); }
+constexpr bool variant_has_group(int smax, int G)
+{
+    return snr_group(variant_pmin(smax)) <= G && G <= snr_group(variant_pmax(smax));
+}
+
+template <int SMAX>
 __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& U, float* data, int q, const int* wl,
                                              int nrows, int tid, float* whb, unsigned long long* tl)
 {
@@ -1096,15 +1113,30 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
     float* snr = a.snr + (uint64_t)U.trial * a.snr_stride + (U.snr_row + (uint64_t)U.s0) * (uint64_t)nw;
     if (c <= kSnrMaxChunk) {
         // short rows (p <= 40 / 72): register chunks sized to the row, not 17
-        if (G == 8 && c <= 5) snr_rows<5, 8>(a, U, data, q, wl, nev, c, tid, whb, tl);
-        else if (G == 8 && c <= 9) snr_rows<9, 8>(a, U, data, q, wl, nev, c, tid, whb, tl);
-        else if (G == 8) snr_rows<kSnrMaxChunk, 8>(a, U, data, q, wl, nev, c, tid, whb, tl);
-        else if (G == 16) snr_rows<kSnrMaxChunk, 16>(a, U, data, q, wl, nev, c, tid, whb, tl);
-        else if (G == 32) snr_rows<kSnrMaxChunk, 32>(a, U, data, q, wl, nev, c, tid, whb, tl);
-        else snr_rows<kSnrMaxChunk, 64>(a, U, data, q, wl, nev, c, tid, whb, tl);
+        if constexpr (variant_has_group(SMAX, 8)) {
+            if (G == 8) {
+                if (c <= 5) snr_rows<5, 8>(a, U, data, q, wl, nev, c, tid, whb, tl);
+                else if (c <= 9) snr_rows<9, 8>(a, U, data, q, wl, nev, c, tid, whb, tl);
+                else snr_rows<kSnrMaxChunk, 8>(a, U, data, q, wl, nev, c, tid, whb, tl);
+                return;
+            }
+        }
+        if constexpr (variant_has_group(SMAX, 16)) {
+            if (G == 16) {
+                snr_rows<kSnrMaxChunk, 16>(a, U, data, q, wl, nev, c, tid, whb, tl);
+                return;
+            }
+        }
+        if constexpr (variant_has_group(SMAX, 32)) {
+            if (G == 32) {
+                snr_rows<kSnrMaxChunk, 32>(a, U, data, q, wl, nev, c, tid, whb, tl);
+                return;
+            }
+        }
+        if constexpr (variant_has_group(SMAX, 64)) snr_rows<kSnrMaxChunk, 64>(a, U, data, q, wl, nev, c, tid, whb, tl);
     } else if (c <= kSnrChunk) {
-        snr_rows<kSnrChunk, 64>(a, U, data, q, wl, nev, c, tid, whb, tl);
-    } else {
+        if constexpr (variant_has_group(SMAX, 64)) snr_rows<kSnrChunk, 64>(a, U, data, q, wl, nev, c, tid, whb, tl);
+    } else if constexpr (variant_pmax(SMAX) > 64 * kSnrChunk) {
         // very wide rows (p > 64 * kSnrChunk): one wave per row, chunks from LDS
         const int g = lane;
         const int j0 = min(g * c, p);
@@ -1240,9 +1272,9 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
         }
     } else {
 #ifdef RT_STAMPS
-        if (!(a.flags & kConeDiagNoSnr)) snr_epilogue(a, U, obuf, ostride, wl, n0, tid, whb, tl);
+        if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX>(a, U, obuf, ostride, wl, n0, tid, whb, tl);
 #else
-        if (!(a.flags & kConeDiagNoSnr)) snr_epilogue(a, U, obuf, ostride, wl, n0, tid, whb, nullptr);
+        if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX>(a, U, obuf, ostride, wl, n0, tid, whb, nullptr);
 #endif
     }
 #ifdef RT_STAMPS
