@@ -85,11 +85,17 @@ RT_HD constexpr int row_pack(int smax) { return smax == kPack2 ? 2 : 1; }
 
 // Register rows per wave the merge stages for a variant (register budget);
 // each register row holds row_pack(smax) output rows.
+#ifndef RT_RW4
+#define RT_RW4 9   // register rows per wave of the 4-slot variant: 9 x 8 waves = 72 rows = its LDS capacity at p >= 242 (the register budget would allow 11; the 2 extra register rows would be computed and dropped on every level)
+#endif
 RT_HD constexpr int merge_rows_per_wave(int smax)
 {
-    return kStageRegs / slot_count(smax) < 1
-               ? 1
-               : (kStageRegs / slot_count(smax) < kMaxRowsPerWave ? kStageRegs / slot_count(smax) : kMaxRowsPerWave);
+    return (smax == 4 && RT_RW4 > 0)
+               ? RT_RW4
+               : (kStageRegs / slot_count(smax) < 1
+                      ? 1
+                      : (kStageRegs / slot_count(smax) < kMaxRowsPerWave ? kStageRegs / slot_count(smax)
+                                                                         : kMaxRowsPerWave));
 }
 
 // Row capacity of one cone work unit for p phase bins run by the kernel
