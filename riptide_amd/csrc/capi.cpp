@@ -203,8 +203,7 @@ void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStrea
         a.items = P.d_units + L.first;
         a.num_items = L.count;
         const uint64_t units = (uint64_t)L.count * batch;   // one workgroup per (item, trial)
-        if (units > 0x7FFFFFFFull) throw std::invalid_argument("too many cone work units in one launch");
-        const uint32_t grid = (uint32_t)units;
+        if (L.count > 0x7FFFFFFFu || batch > 65535u) throw std::invalid_argument("too many cone work units in one launch");
         // diagnostic builds: this launch's unit records follow the previous ones
         a.stamps = nullptr;
         if (g_stamps && g_stamp_units + units <= kTimelineCap) {
@@ -219,7 +218,7 @@ void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStrea
             r.moved = L.moved_bytes * batch;
             ck(hipEventRecord(r.a, s), "hipEventRecord");
         }
-        ck(launch_cone(a, grid, L.smax, s), "cone_kernel");
+        ck(launch_cone(a, L.smax, s), "cone_kernel");
         if (g_prof.on) {
             ck(hipEventRecord(r.b, s), "hipEventRecord");
             g_prof.rec[0].push_back(r);

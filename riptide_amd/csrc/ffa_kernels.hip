@@ -290,11 +290,10 @@ __device__ __forceinline__ UnitView unit_view(const ConeArgs& a, int item, int t
 
 // Metadata of unit u into M (+ the source-row table of its bottom level).
 // Every thread calls it; it ends with a barrier.
-__device__ __forceinline__ void setup_unit(const ConeArgs& a, int u, UnitMeta& M, int* src_row, int tid)
+__device__ __forceinline__ void setup_unit(const ConeArgs& a, int item, int trial, UnitMeta& M, int* src_row, int tid)
 {
     const int lane = tid & 63, wave = tid >> 6;
-    const int batch = (int)a.batch;
-    const UnitView U = unit_view(a, u / batch, u % batch);
+    const UnitView U = unit_view(a, item, trial);
     if (tid == 0) M.view = U;
     const int L = U.levels;
     if (U.mode == kModeTile) {
@@ -467,6 +466,17 @@ __device__ __forceinline__ void fill_land(const Fill& F, float* base)
 // Row descriptor (head row, tail row, roll shift) of output row r at level
 // l, as row indices of the level below; t = -1 for a carried leaf (size-1
 // node).
+// x mod p for 0 <= x < 2^22 and p >= 1 (roll shifts: x = s - t(s) < node
+// size): a float-reciprocal quotient, off by at most one, then corrected --
+// ~8 VALU instead of the ~35 of an integer remainder by a run-time p.
+__device__ __forceinline__ int mod_small(int x, int p)
+{
+    const int q = (int)((float)x * __builtin_amdgcn_rcpf((float)p));
+    int r = x - (int)__umul24((unsigned)q, (unsigned)p);
+    r = r < 0 ? r + p : r;
+    return r >= p ? r - p : r;
+}
+
 __device__ __forceinline__ void row_desc(const UnitMeta& M, bool tile, int node_size, int l, int r, int p, int& h,
                                          int& t, int& sh)
 {
@@ -486,7 +496,7 @@ __device__ __forceinline__ void row_desc(const UnitMeta& M, bool tile, int node_
         const int tt = (int)merge_index(merge_coef(ts, (uint32_t)R.size), (uint32_t)u);
         h = H.base + hh - H.lo;
         t = T.base + tt - T.lo;
-        sh = (u - tt) % p;
+        sh = mod_small(u - tt, p);
     } else {
         int a0 = 0, sz = node_size;
         for (int d = 0; d < l; ++d) {
@@ -510,7 +520,7 @@ __device__ __forceinline__ void row_desc(const UnitMeta& M, bool tile, int node_
             const int tt = (int)merge_index(merge_coef(ts, (uint32_t)sz), (uint32_t)s);
             h = a0 + hh;
             t = a0 + (int)hs + tt;
-            sh = (s - tt) % p;
+            sh = mod_small(s - tt, p);
         }
     }
 }
@@ -1214,10 +1224,13 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
     __shared__ float whb[2 * kMaxWidths];   // S/N: h + b and b per width
 
     const int tid = threadIdx.x;
-    const int u = (int)blockIdx.x;
-    if (u >= (int)(a.num_items * a.batch)) return;
+    // grid (items, trials): no division to split a flat unit index
+    const int item = (int)blockIdx.x, trial = (int)blockIdx.y;
+    if (item >= (int)a.num_items || trial >= (int)a.batch) return;
+    const int u = trial * (int)a.num_items + item;   // unit record index (diagnostic stamps)
+    (void)u;
     if (tid < (int)a.num_widths) wl[tid] = (int)a.widths[tid];   // visible after setup's barriers
-    setup_unit(a, u, M, src_row, tid);
+    setup_unit(a, item, trial, M, src_row, tid);
     RT_MARK(1);
     const UnitView U = read_view(M);
     const int p = U.p;
@@ -1293,10 +1306,10 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
 #endif
 }
 
-hipError_t launch_cone(const ConeArgs& args, uint32_t grid, uint32_t smax, hipStream_t s)
+hipError_t launch_cone(const ConeArgs& args, uint32_t smax, hipStream_t s)
 {
-    if (!args.num_items || !args.batch || !grid) return hipSuccess;
-    const dim3 g(grid), b(kConeBlock);
+    if (!args.num_items || !args.batch) return hipSuccess;
+    const dim3 g(args.num_items, args.batch), b(kConeBlock);
     switch (smax) {
     case 1: hipLaunchKernelGGL(cone_kernel<1>, g, b, 0, s, args); break;
     case 2: hipLaunchKernelGGL(cone_kernel<2>, g, b, 0, s, args); break;
