@@ -218,7 +218,7 @@ void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStrea
             r.moved = L.moved_bytes * batch;
             ck(hipEventRecord(r.a, s), "hipEventRecord");
         }
-        ck(launch_cone(a, L.smax, s), "cone_kernel");
+        ck(launch_cone(a, L.smax, L.rw, s), "cone_kernel");
         if (g_prof.on) {
             ck(hipEventRecord(r.b, s), "hipEventRecord");
             g_prof.rec[0].push_back(r);

@@ -1209,9 +1209,10 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
 // One kernel per merge slot width SMAX (units with ceil(p/64) <= SMAX), so each
 // gets its own register allocation.  min 4 waves per SIMD: <= 128 VGPRs, two
 // workgroups per CU.
-template <int SMAX>
+template <int SMAX, int RWT = 0>
 __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(ConeArgs a)
 {
+    constexpr int RW = RWT ? RWT : merge_rows_per_wave(SMAX);   // register rows per wave
 #ifdef RT_STAMPS
     unsigned long long tl[kStampMarks] = {};
     tl[0] = __builtin_amdgcn_s_memtime();
@@ -1241,7 +1242,9 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
     // (kPack2 runs exactly the p <= 32 rows)
     ok = ok && ((SMAX <= 5 || SMAX == kPack2) ? merge_slots((uint32_t)p) == SMAX
                                               : (merge_slots((uint32_t)p) <= SMAX && merge_slots((uint32_t)p) != kPack2));
-    for (int l = 0; l <= L; ++l) ok = ok && uni(M.nrows[l]) <= lds_row_capacity((uint32_t)p, SMAX);
+    for (int l = 0; l <= L; ++l)
+        ok = ok && uni(M.nrows[l]) <= lds_row_capacity((uint32_t)p, SMAX) &&
+             uni(M.nrows[l]) <= kConeWaves * RW * row_pack(SMAX);
     if (!ok) {
         if (tid == 0 && a.error_flag) atomicOr(a.error_flag, 1);
         return;
@@ -1268,7 +1271,7 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
     const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(dst, (((uint32_t)U.m * (uint32_t)p + 3u) & ~3u) * 4u);
     const uint32_t o0 = (uint32_t)(U.node_start + U.s0) * (uint32_t)p * 4u;
     if (L > 0 && !(a.flags & kConeDiagNoMerge))
-        merge_levels<SMAX, merge_rows_per_wave(SMAX)>(M, base, desc, use_table, p, L, tile, U.node_size, tid, st_regs,
+        merge_levels<SMAX, RW>(M, base, desc, use_table, p, L, tile, U.node_size, tid, st_regs,
                                                       rs, o0, a.flags, data + kLdsDataFloats + 4 + (tid & 63));
     RT_MARK(5);
     const int n0 = uni(M.nrows[0]);
@@ -1306,7 +1309,7 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
 #endif
 }
 
-hipError_t launch_cone(const ConeArgs& args, uint32_t smax, hipStream_t s)
+hipError_t launch_cone(const ConeArgs& args, uint32_t smax, uint32_t rw, hipStream_t s)
 {
     if (!args.num_items || !args.batch) return hipSuccess;
     const dim3 g(args.num_items, args.batch), b(kConeBlock);
@@ -1314,8 +1317,24 @@ hipError_t launch_cone(const ConeArgs& args, uint32_t smax, hipStream_t s)
     case 1: hipLaunchKernelGGL(cone_kernel<1>, g, b, 0, s, args); break;
     case 2: hipLaunchKernelGGL(cone_kernel<2>, g, b, 0, s, args); break;
     case 3: hipLaunchKernelGGL(cone_kernel<3>, g, b, 0, s, args); break;
-    case 4: hipLaunchKernelGGL(cone_kernel<4>, g, b, 0, s, args); break;
-    case 5: hipLaunchKernelGGL(cone_kernel<5>, g, b, 0, s, args); break;
+    case 4:
+        switch (rw) {
+        case 5: hipLaunchKernelGGL((cone_kernel<4, 5>), g, b, 0, s, args); break;
+        case 6: hipLaunchKernelGGL((cone_kernel<4, 6>), g, b, 0, s, args); break;
+        case 7: hipLaunchKernelGGL((cone_kernel<4, 7>), g, b, 0, s, args); break;
+        case 8: hipLaunchKernelGGL((cone_kernel<4, 8>), g, b, 0, s, args); break;
+        default: hipLaunchKernelGGL(cone_kernel<4>, g, b, 0, s, args); break;
+        }
+        break;
+    case 5:
+        switch (rw) {
+        case 5: hipLaunchKernelGGL((cone_kernel<5, 5>), g, b, 0, s, args); break;
+        case 6: hipLaunchKernelGGL((cone_kernel<5, 6>), g, b, 0, s, args); break;
+        case 7: hipLaunchKernelGGL((cone_kernel<5, 7>), g, b, 0, s, args); break;
+        case 8: hipLaunchKernelGGL((cone_kernel<5, 8>), g, b, 0, s, args); break;
+        default: hipLaunchKernelGGL(cone_kernel<5>, g, b, 0, s, args); break;
+        }
+        break;
     case 8: hipLaunchKernelGGL(cone_kernel<8>, g, b, 0, s, args); break;
     case 16: hipLaunchKernelGGL(cone_kernel<16>, g, b, 0, s, args); break;
     case kMaxSlots: hipLaunchKernelGGL(cone_kernel<kMaxSlots>, g, b, 0, s, args); break;
