@@ -4,6 +4,7 @@
 #include "plan.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <stdexcept>
 
@@ -166,6 +167,19 @@ static bool fits(const ConeNeed& n, uint32_t p, int smax)
 // Per-transform schedule: list of passes, each a list of (node, tile, levels).
 struct PassItems { std::vector<ConeItem> items; double read = 0, written = 0; };
 
+// Tile-level cost model: a pass costs C / (C - cone overhead) merge units plus
+// pass_weight() for its HBM round trip and unit setup (RIPTIDE_AMD_PASS_WEIGHT).
+// Measured (cfg2, ms per trial): weight 1 -> 11.57, 20 -> 11.47, 100 -> 11.43:
+// fewer passes win even at a larger cone overhead, so the default is 100.
+static double pass_weight()
+{
+    if (const char* e = std::getenv("RIPTIDE_AMD_PASS_WEIGHT")) {
+        const double v = std::atof(e);
+        if (v >= 0) return v;
+    }
+    return 100.0;
+}
+
 static void plan_transform(const FfaXform& X, uint32_t xi, int smax, std::vector<PassItems>& passes)
 {
     passes.clear();
@@ -201,7 +215,7 @@ static void plan_transform(const FfaXform& X, uint32_t xi, int smax, std::vector
         const int extra = 2 << L;
         if (extra + 1 >= C) break;
         const int npass = (db + L - 1) / L;
-        const double cost = npass * ((double)C / (double)(C - extra) + 1.0);
+        const double cost = npass * ((double)C / (double)(C - extra) + pass_weight());
         if (cost < best - 1e-9) { best = cost; bestL = L; }
     }
     const int npass = (db + bestL - 1) / bestL;
