@@ -1314,7 +1314,14 @@ hipError_t launch_cone(const ConeArgs& args, uint32_t smax, uint32_t rw, hipStre
     if (!args.num_items || !args.batch) return hipSuccess;
     const dim3 g(args.num_items, args.batch), b(kConeBlock);
     switch (smax) {
-    case 1: hipLaunchKernelGGL(cone_kernel<1>, g, b, 0, s, args); break;
+    case 1:
+        switch (rw) {
+        case 12: hipLaunchKernelGGL((cone_kernel<1, 12>), g, b, 0, s, args); break;
+        case 16: hipLaunchKernelGGL((cone_kernel<1, 16>), g, b, 0, s, args); break;
+        case 20: hipLaunchKernelGGL((cone_kernel<1, 20>), g, b, 0, s, args); break;
+        default: hipLaunchKernelGGL(cone_kernel<1>, g, b, 0, s, args); break;
+        }
+        break;
     case 2: hipLaunchKernelGGL(cone_kernel<2>, g, b, 0, s, args); break;
     case 3: hipLaunchKernelGGL(cone_kernel<3>, g, b, 0, s, args); break;
     case 4:

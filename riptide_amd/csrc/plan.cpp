@@ -343,12 +343,14 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
                                      return item_cost(x, out.xf[x.xform]) > item_cost(y, out.xf[y.xform]);
                                  });
                 if (!L.count) continue;
-                if (k == 0 && (bucket == 4 || bucket == 5) && merge_rows_per_wave(bucket) > kMinRw) {
+                if (k == 0 && (bucket == 1 || bucket == 4 || bucket == 5) && merge_rows_per_wave(bucket) > kMinRw) {
                     // whole-node pass: one launch per register-row class
-                    // ceil(node rows / 8) (bytes split by cells)
+                    // ceil(node rows / 8) (bytes split by cells); the 1-slot
+                    // variant (24 rows) in classes of 4 rows from 12
                     const int rwd = merge_rows_per_wave(bucket);
                     auto rw_of = [&](const ConeItem& x) {
-                        const int r = ((int)x.node_size + kConeWaves - 1) / kConeWaves;
+                        int r = ((int)x.node_size + kConeWaves - 1) / kConeWaves;
+                        if (bucket == 1) r = r <= 12 ? 12 : (r + 3) / 4 * 4;
                         return r < kMinRw ? kMinRw : r;
                     };
                     auto b0 = out.items.begin() + L.first, b1 = out.items.end();
