@@ -891,6 +891,13 @@ int rt_schedule_check(size_t size, double tsamp, size_t nw, double pmin, double 
                 } else if ((int)it.node_size * (int)X.p > kLdsDataFloats || it.node_size > (uint32_t)kMaxRows) {
                     throw std::runtime_error("schedule: whole node exceeds the LDS budget");
                 }
+                // a launch's kernel instance stages enough register rows for every level
+                const int rw = L.rw ? (int)L.rw : merge_rows_per_wave((int)L.smax);
+                const int rows = it.mode == kModeTile
+                                     ? cone_need(it.node_size, it.s0, it.s1, it.levels, X.p).max_rows
+                                     : (int)it.node_size;
+                if (rows > kConeWaves * rw * row_pack((int)L.smax) || rows > lds_row_capacity(X.p, (int)L.smax))
+                    throw std::runtime_error("schedule: unit rows exceed its kernel instance's register rows");
                 if (L.pass == last_pass[it.xform]) {
                     if (it.dst != kSelSnr || it.node_start != 0) throw std::runtime_error("schedule: bad final pass");
                     covered[it.xform] += it.s1 - it.s0;
