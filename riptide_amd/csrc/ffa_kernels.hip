@@ -398,12 +398,12 @@ __device__ __forceinline__ void fill_issue(const ConeArgs& a, const UnitMeta& M,
             const int c = tid + k * kConeBlock;
             F.lo[k] = 0;
             F.e[k] = c < nchunks ? 4 * c - al : n;
-            if (c < nchunks) {
-                const uint32_t off = (g0 - (uint32_t)al + 4u * (uint32_t)c) * 4u;
-                const auto q = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
-                F.v[k] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]),
-                                     __uint_as_float(q[3]));
-            }
+            // chunks past the level load from an out-of-range offset (the
+            // buffer returns zeros; never landed): no exec-mask branch
+            const uint32_t off = c < nchunks ? (g0 - (uint32_t)al + 4u * (uint32_t)c) * 4u : 0x80000000u;
+            const auto q = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
+            F.v[k] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]),
+                                 __uint_as_float(q[3]));
         }
     } else {
         const int amax = (p & 3) == 0 ? 0 : ((p & 1) == 0 ? 2 : 3);
@@ -423,12 +423,10 @@ __device__ __forceinline__ void fill_issue(const ConeArgs& a, const UnitMeta& M,
             const int e = 4 * c - al;
             F.lo[k] = rr * p;
             F.e[k] = on ? e : p;
-            if (on && e < p) {
-                const uint32_t off = (g - (uint32_t)al + 4u * (uint32_t)c) * 4u;
-                const auto q = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
-                F.v[k] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]),
-                                     __uint_as_float(q[3]));
-            }
+            const uint32_t off = (on && e < p) ? (g - (uint32_t)al + 4u * (uint32_t)c) * 4u : 0x80000000u;
+            const auto q = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
+            F.v[k] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]),
+                                 __uint_as_float(q[3]));
             r += dr;
             c += dc;
             if (c >= nch) {
