@@ -139,6 +139,15 @@ int rt_periodogram_device(const rt_plan* plan, const float* d_data, size_t batch
                           float* d_snrs, size_t snr_stride, void* d_workspace, size_t workspace_bytes,
                           void* stream);
 
+/* Device error flag of a plan: the cone kernel refuses (and leaves unwritten)
+ * any work unit that breaks its LDS / register budget and raises the plan's
+ * sticky flag.  Reads it on `stream` (synchronising that stream), clears it,
+ * and returns RT_EINTERNAL if it was set.  The reference has no such state
+ * (a CPU transform cannot run out of LDS); the host entry point
+ * rt_periodogram checks it itself, as riptide::periodogram
+ * (periodogram.hpp:117-201) would raise. */
+int rt_plan_check(const rt_plan* plan, void* stream);
+
 /* Device workspace bytes for rt_deredden_normalise_device. */
 int rt_deredden_workspace_bytes(size_t size, size_t width_samples, size_t min_points, size_t batch,
                                 size_t* bytes);

@@ -1,18 +1,26 @@
 """CPU baseline for bench.py (TEST INFRASTRUCTURE, run in a subprocess).
 
-Times one DM trial of the bench workload through the reference's CPU path:
-the reference C++ periodogram (oracle/_ref/portable, built from the reference
-sources with its own flags but a portable ISA) when present -> kind
-"reference", otherwise the clean-room C restatement -> kind "port"; plus the
-numpy dereddening/normalisation restated in oracle.py.  One process, one core
-(threadpoolctl-style BLAS limits are irrelevant: no BLAS is used).
+The rffa CPU model (riptide/pipeline/worker_pool.py:35-45 and
+pipeline.py:508): a multiprocessing.Pool of C worker processes, one DM trial
+per process, BLAS pinned to one thread; each trial is dereddened and
+normalised (numpy, restated in oracle.py from time_series.py:66-122), then
+searched by the reference C++ periodogram built from the reference sources
+with its own flags (oracle/_ref/v4 = -march=x86-64-v4 on AVX-512 hosts,
+oracle/_ref/portable = x86-64-v3 otherwise -> kind "reference"; the clean-room
+C restatement when neither is present -> kind "port"), then run through
+find_peaks (riptide_amd.peak_detection, the reference's numpy expressions).
 
-Prints one JSON object.
+C = the worker processes actually used: the CPU share this process may use
+(sched_getaffinity, capped by OMP_NUM_THREADS where the harness sets it, as on
+the GPU box: 16 host cores per GPU).  Reports the search-only rate (deredden
++ normalise + periodogram: the work bench.py's GPU step does) as `value`, and
+search + find_peaks separately.  Prints one JSON object.
 """
 import argparse
 import glob
 import importlib.util
 import json
+import multiprocessing
 import os
 import sys
 import time
@@ -24,8 +32,65 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path = [p for p in sys.path if os.path.abspath(p or '.') != HERE]
 sys.path.insert(0, os.path.dirname(HERE))
 
+_A = None            # parsed arguments (inherited by the forked workers)
+_PGRAM = None
+_KIND = None
+
+
+def _avx512():
+    try:
+        with open("/proc/cpuinfo") as f:
+            return any(l.startswith("flags") and " avx512f" in l for l in f)
+    except OSError:
+        return False
+
+
+def _load_pgram():
+    from oracle import oracle as O
+    for sub in (["v4"] if _avx512() else []) + ["portable"]:
+        so = glob.glob(os.path.join(HERE, "_ref", sub, "libcpp*.so"))
+        if so:
+            try:
+                spec = importlib.util.spec_from_file_location("libcpp", so[0])
+                mod = importlib.util.module_from_spec(spec)
+                spec.loader.exec_module(mod)
+                return mod.periodogram, "reference", f"reference C++ (-O3 -ffast-math, {sub} build)"
+            except Exception:
+                pass
+    O.build()
+    return (lambda d, ts, w, p0, p1, b0, b1: O.periodogram(d, ts, w, p0, p1, b0, b1)), "port", "oracle C restatement"
+
+
+def _trial(k):
+    """One DM trial (process_fname model): returns absolute timestamps
+    (start, search done, peaks done) after the untimed input generation."""
+    from oracle import oracle as O
+    from riptide_amd.peak_detection import find_peaks
+    from riptide_amd.periodogram import Periodogram
+    a = _A
+    raw = np.random.RandomState(1234 + k).normal(size=a.n).astype(np.float32)
+    widths = O.generate_width_trials(a.bmin, a.ducy_max)
+    t0 = time.time()
+    x = O.normalise(O.deredden(raw, a.tsamp, 4.0, 101))
+    periods, foldbins, snrs = _PGRAM(x, a.tsamp, widths, a.pmin, a.pmax, a.bmin, a.bmax)
+    t1 = time.time()
+    pg = Periodogram(widths, periods, foldbins, snrs, metadata={"tobs": a.n * a.tsamp, "dm": float(k)})
+    find_peaks(pg)
+    t2 = time.time()
+    return t0, t1, t2
+
+
+def default_cores():
+    c = len(os.sched_getaffinity(0))
+    for var in ("OMP_NUM_THREADS",):
+        v = os.environ.get(var)
+        if v and v.isdigit() and int(v) > 0:
+            c = min(c, int(v))
+    return c
+
 
 def main():
+    global _A, _PGRAM, _KIND
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1 << 23)
     ap.add_argument("--tsamp", type=float, default=256e-6)
@@ -34,37 +99,29 @@ def main():
     ap.add_argument("--bmin", type=int, default=240)
     ap.add_argument("--bmax", type=int, default=260)
     ap.add_argument("--ducy-max", type=float, default=0.05)
-    ap.add_argument("--trials", type=int, default=1)
-    a = ap.parse_args()
-    from oracle import oracle as O
-    so = glob.glob(os.path.join(HERE, "_ref", "portable", "libcpp*.so"))
-    kind = "port"
-    pgram = None
-    if so:
-        try:
-            spec = importlib.util.spec_from_file_location("libcpp", so[0])
-            mod = importlib.util.module_from_spec(spec)
-            spec.loader.exec_module(mod)
-            pgram = mod.periodogram
-            kind = "reference"
-        except Exception:
-            pgram = None
-    if pgram is None:
-        O.build()
-        pgram = lambda d, ts, w, p0, p1, b0, b1: O.periodogram(d, ts, w, p0, p1, b0, b1)  # noqa: E731
-    widths = O.generate_width_trials(a.bmin, a.ducy_max)
-    rs = np.random.RandomState(1234)
-    t_total = 0.0
-    for _ in range(a.trials):
-        raw = rs.normal(size=a.n).astype(np.float32)
-        t0 = time.perf_counter()
-        x = O.normalise(O.deredden(raw, a.tsamp, 4.0, 101))
-        pgram(x, a.tsamp, widths, a.pmin, a.pmax, a.bmin, a.bmax)
-        t_total += time.perf_counter() - t0
-    print(json.dumps({"value": a.trials / t_total, "unit": "DM trials/s", "cores": 1, "kind": kind,
-                      "sample": f"{a.trials} trial(s) of {a.n} samples: numpy deredden+normalise + "
-                                f"{'reference C++ (-O3 -ffast-math -march=x86-64-v3)' if kind == 'reference' else 'oracle C'} "
-                                f"periodogram, 1 process", "seconds": t_total}))
+    ap.add_argument("--cores", type=int, default=0, help="worker processes (default: this process's CPU share)")
+    ap.add_argument("--trials-per-core", type=int, default=1)
+    _A = ap.parse_args()
+    cores = _A.cores or default_cores()
+    for var in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):   # threadpool_limits(1)
+        os.environ[var] = "1"
+    ntrials = cores * _A.trials_per_core
+    _PGRAM, _KIND, what = _load_pgram()
+    ctx = multiprocessing.get_context("fork")
+    with ctx.Pool(processes=cores) as pool:
+        stamps = pool.map(_trial, range(ntrials), chunksize=1)
+    start = min(s[0] for s in stamps)
+    search_wall = max(s[1] for s in stamps) - start
+    total_wall = max(s[2] for s in stamps) - start
+    print(json.dumps({
+        "value": ntrials / search_wall, "unit": "DM trials/s", "cores": cores, "kind": _KIND,
+        "search_and_peaks_per_s": ntrials / total_wall,
+        "per_core_search_per_s": ntrials / search_wall / cores,
+        "sample": f"{ntrials} cfg2 trial(s) of {_A.n} samples, multiprocessing.Pool({cores}) one trial per "
+                  f"process (rffa worker-pool model): numpy deredden+normalise + {what} periodogram = value; "
+                  f"+ find_peaks = search_and_peaks_per_s; host CPU share {len(os.sched_getaffinity(0))} "
+                  f"affinity cores",
+        "seconds": total_wall}))
 
 
 if __name__ == "__main__":

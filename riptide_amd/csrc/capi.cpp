@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -131,8 +132,11 @@ struct ProfRec {
     hipEvent_t a, b;
     double alg, moved;
 };
+// One profiler per process, shared by every host thread (one per GPU is the
+// supported model): `mu` guards the record lists and the event pool.
 struct Profiler {
-    bool on = false;
+    std::mutex mu;
+    std::atomic<bool> on{false};
     std::vector<ProfRec> rec[2];
     std::vector<hipEvent_t> pool;
     hipEvent_t ev()
@@ -182,6 +186,16 @@ struct DevicePlan {
             d.dst = it.dst;
             u[i] = d;
         }
+        // Test hook (RIPTIDE_AMD_DEBUG_CORRUPT_UNIT=1): give the first whole-node
+        // unit 4096 rows after the host validation, so the kernel's own budget
+        // check refuses it and sets the error flag (exercises rt_plan_check).
+        if (const char* e = std::getenv("RIPTIDE_AMD_DEBUG_CORRUPT_UNIT"))
+            if (std::atoi(e) != 0)
+                for (UnitDesc& d : u)
+                    if (d.mode == kModeWhole) {
+                        d.node_size = 4096;
+                        break;
+                    }
         ck(hipMalloc(&d_units, std::max<size_t>(1, u.size()) * sizeof(UnitDesc)), "hipMalloc");
         if (!u.empty())
             ck(hipMemcpy(d_units, u.data(), u.size() * sizeof(UnitDesc), hipMemcpyHostToDevice), "upload units");
@@ -206,32 +220,43 @@ void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStrea
         if (L.count > 0x7FFFFFFFu || batch > 65535u) throw std::invalid_argument("too many cone work units in one launch");
         // diagnostic builds: this launch's unit records follow the previous ones
         a.stamps = nullptr;
-        if (g_stamps && g_stamp_units + units <= kTimelineCap) {
-            a.stamps = g_stamps + g_stamp_units * kStampRecWords;
-            g_stamp_units += units;
+        if (g_stamps) {
+            std::lock_guard<std::mutex> lk(g_prof.mu);
+            if (g_stamp_units + units <= kTimelineCap) {
+                a.stamps = g_stamps + g_stamp_units * kStampRecWords;
+                g_stamp_units += units;
+            }
         }
         ProfRec r{};
-        if (g_prof.on) {
-            r.a = g_prof.ev();
-            r.b = g_prof.ev();
+        const bool prof = g_prof.on;
+        if (prof) {
+            {
+                std::lock_guard<std::mutex> lk(g_prof.mu);
+                r.a = g_prof.ev();
+                r.b = g_prof.ev();
+            }
             r.alg = L.alg_bytes * batch;
             r.moved = L.moved_bytes * batch;
             ck(hipEventRecord(r.a, s), "hipEventRecord");
         }
         ck(launch_cone(a, L.smax, L.rw, s), "cone_kernel");
-        if (g_prof.on) {
+        if (prof) {
             ck(hipEventRecord(r.b, s), "hipEventRecord");
+            std::lock_guard<std::mutex> lk(g_prof.mu);
             g_prof.rec[0].push_back(r);
         }
     }
 }
 
 // Single-transform FFA (ffa2 / benchmark_ffa2): in (device) -> out (device).
-void ffa_device(const float* d_in, size_t rows, size_t cols, float* d_out, float* d_tmp, hipStream_t s,
+// d_flag: device int the cone kernel sets if a unit breaks its budget (the
+// caller checks it after synchronising).  A plan built here is freed only
+// after the stream has drained; a cached plan lives in the caller.
+void ffa_device(const float* d_in, size_t rows, size_t cols, float* d_out, float* d_tmp, int* d_flag, hipStream_t s,
                 DevicePlan* cached = nullptr)
 {
     if (!rows || !cols) return;
-    if (lds_row_capacity((uint32_t)cols) >= 3) {
+    if (lds_row_capacity((uint32_t)cols) >= 3 && (uint64_t)rows * cols * 4u < kMaxBlockBytes) {
         DevicePlan local;
         DevicePlan& P = cached ? *cached : local;
         if (!cached || P.ex.launches.empty()) {
@@ -245,9 +270,9 @@ void ffa_device(const float* d_in, size_t rows, size_t cols, float* d_out, float
         a.leaves = d_in;
         a.ping = d_out;
         a.pong = d_tmp;
-        int* flag = nullptr;
-        a.error_flag = flag;
+        a.error_flag = d_flag;
         run_cone_launches(P, a, 1, s);
+        if (!cached) sync(s);   // `local` (and its unit table) is freed on return
         return;
     }
     // rows too wide for LDS: per-depth global-memory passes
@@ -299,10 +324,12 @@ struct rt_plan {
     DsRung* d_rungs = nullptr;
     uint32_t ds_blocks = 0;
     bool ds_fused = false;   // every rung fits the fused ladder's margin
+    int* d_flag = nullptr;   // sticky device error flag of the cone kernel (rt_plan_check reads and clears it)
     ~rt_plan()
     {
         if (d_rungs) (void)hipFree(d_rungs);
         if (d_widths) (void)hipFree(d_widths);
+        if (d_flag) (void)hipFree(d_flag);
     }
 };
 
@@ -346,6 +373,8 @@ rt_plan* make_plan(size_t size, double tsamp, const uint64_t* widths, size_t nw,
         // scratch budget per ping/pong buffer and trial (scratch_budget_floats)
         build_exec_plan(xf, true, (uint32_t)nw, scratch_budget_floats(), P->dp.ex);
         P->dp.upload();
+        ck(hipMalloc(&P->d_flag, sizeof(int)), "hipMalloc");
+        ck(hipMemset(P->d_flag, 0, sizeof(int)), "hipMemset");
         // downsample ladder over the rungs that feed at least one transform
         std::vector<bool> used(P->pg.rungs.size(), false);
         for (const FfaXform& X : xf) used[X.rung] = true;
@@ -382,7 +411,7 @@ size_t plan_ws_bytes(const rt_plan* P, size_t batch)
 {
     size_t b = align_up(P->pg.leaf_floats * 4 * batch, 256);
     b += 2 * align_up(P->dp.ex.scratch_floats * 4 * batch, 256);
-    b += 256;   // error flag
+    b += 256;   // slack
     return b;
 }
 
@@ -396,13 +425,14 @@ void run_periodogram(const rt_plan* P, const float* d_data, size_t batch, size_t
     float* ping = (float*)w;
     w += align_up(P->dp.ex.scratch_floats * 4 * batch, 256);
     float* pong = (float*)w;
-    w += align_up(P->dp.ex.scratch_floats * 4 * batch, 256);
-    int* flag = (int*)w;
-    ck(hipMemsetAsync(flag, 0, sizeof(int), s), "hipMemsetAsync");
     ProfRec r{};
-    if (g_prof.on) {
-        r.a = g_prof.ev();
-        r.b = g_prof.ev();
+    const bool prof = g_prof.on;
+    if (prof) {
+        {
+            std::lock_guard<std::mutex> lk(g_prof.mu);
+            r.a = g_prof.ev();
+            r.b = g_prof.ev();
+        }
         ck(hipEventRecord(r.a, s), "hipEventRecord");
     }
     if (P->ds_fused)
@@ -413,12 +443,13 @@ void run_periodogram(const rt_plan* P, const float* d_data, size_t batch, size_t
         ck(launch_downsample_ladder(d_data, P->pg.prm.size, data_stride, P->d_rungs, (uint32_t)P->rungs.size(),
                                     P->ds_blocks, leaves, P->pg.leaf_floats, (uint32_t)batch, s),
            "downsample_ladder");
-    if (g_prof.on) {
+    if (prof) {
         ck(hipEventRecord(r.b, s), "hipEventRecord");
         double bytes = P->ds_fused ? 4.0 * P->pg.prm.size : 0.0;   // fused: the series is read once
         for (const DsRung& d : P->rungs)
             bytes += 4.0 * (double)d.n + (P->ds_fused ? 0.0 : (d.identity ? 4.0 * d.n : 4.0 * P->pg.prm.size));
         r.alg = r.moved = bytes * batch;
+        std::lock_guard<std::mutex> lk(g_prof.mu);
         g_prof.rec[1].push_back(r);
     }
     ConeArgs a{};
@@ -431,7 +462,7 @@ void run_periodogram(const rt_plan* P, const float* d_data, size_t batch, size_t
     a.buf_stride = P->dp.ex.scratch_floats;
     a.snr = d_snrs;
     a.snr_stride = snr_stride;
-    a.error_flag = flag;
+    a.error_flag = P->d_flag;
     run_cone_launches(P->dp, a, (uint32_t)batch, s);
 }
 
@@ -586,10 +617,15 @@ int rt_ffa2(const float* in, size_t rows, size_t cols, float* out)
         float* dx = dev<float>(c, 0, n);
         float* dz = dev<float>(c, 1, n);
         float* dt = dev<float>(c, 2, n);
+        int* flag = dev<int>(c, 5, 1);
+        ck(hipMemsetAsync(flag, 0, sizeof(int), c.stream), "hipMemsetAsync");
         h2d(dx, in, n * 4, c.stream);
-        ffa_device(dx, rows, cols, dz, dt, c.stream);
+        ffa_device(dx, rows, cols, dz, dt, flag, c.stream);
+        int hflag = 0;
+        d2h(&hflag, flag, sizeof hflag, c.stream);
         d2h(out, dz, n * 4, c.stream);
         sync(c.stream);
+        if (hflag) throw std::runtime_error("cone kernel: work item exceeded the LDS budget");
         return RT_OK;
     });
 }
@@ -605,20 +641,25 @@ int rt_benchmark_ffa2(size_t rows, size_t cols, size_t loops, double* seconds)
         float* dx = dev<float>(c, 0, n);
         float* dz = dev<float>(c, 1, n);
         float* dt = dev<float>(c, 2, n);
+        int* flag = dev<int>(c, 5, 1);
         ck(hipMemsetAsync(dx, 0, n * 4, c.stream), "memset");
+        ck(hipMemsetAsync(flag, 0, sizeof(int), c.stream), "hipMemsetAsync");
         DevicePlan P;
-        ffa_device(dx, rows, cols, dz, dt, c.stream, &P);   // warm-up + plan
+        ffa_device(dx, rows, cols, dz, dt, flag, c.stream, &P);   // warm-up + plan
         hipEvent_t a, b;
         ck(hipEventCreate(&a), "event");
         ck(hipEventCreate(&b), "event");
         ck(hipEventRecord(a, c.stream), "record");
-        for (size_t i = 0; i < loops; ++i) ffa_device(dx, rows, cols, dz, dt, c.stream, &P);
+        for (size_t i = 0; i < loops; ++i) ffa_device(dx, rows, cols, dz, dt, flag, c.stream, &P);
         ck(hipEventRecord(b, c.stream), "record");
         ck(hipEventSynchronize(b), "sync");
         float ms = 0;
         ck(hipEventElapsedTime(&ms, a, b), "elapsed");
         (void)hipEventDestroy(a);
         (void)hipEventDestroy(b);
+        int hflag = 0;
+        ck(hipMemcpy(&hflag, flag, sizeof hflag, hipMemcpyDeviceToHost), "flag");
+        if (hflag) throw std::runtime_error("cone kernel: work item exceeded the LDS budget");
         *seconds = ms * 1e-3 / (double)loops;
         return RT_OK;
     });
@@ -748,8 +789,7 @@ int rt_periodogram(const float* data, size_t size, double tsamp, const uint64_t*
         h2d(dx, data, size * 4, c.stream);
         run_periodogram(P, dx, 1, size, dz, L * nw, ws, plan_ws_bytes(P, 1), c.stream);
         int flag = 0;
-        char* w = (char*)ws + plan_ws_bytes(P, 1) - 256;
-        d2h(&flag, w, sizeof flag, c.stream);
+        d2h(&flag, P->d_flag, sizeof flag, c.stream);
         d2h(snrs, dz, L * nw * 4, c.stream);
         sync(c.stream);
         if (flag) throw std::runtime_error("cone kernel: work item exceeded the LDS budget");
@@ -862,50 +902,16 @@ int rt_schedule_check(size_t size, double tsamp, size_t nw, double pmin, double 
             xf.push_back(X);
         }
         ExecPlan ex;
+        // build_exec_plan validates the schedule (validate_exec_plan: tiles
+        // inside nodes, LDS / register budgets, final pass covers every row)
         build_exec_plan(xf, true, (uint32_t)nw, scratch_budget_floats(), ex);
-        // invariants: within every launch, each transform's items write disjoint
-        // row ranges, every item fits the LDS budget, and the last pass of every
-        // transform covers rows [0, m) exactly once.
-        std::vector<uint64_t> covered(ex.xf.size(), 0);
-        std::vector<uint32_t> last_pass(ex.xf.size(), 0);
-        for (const Launch& L : ex.launches)
-            for (uint32_t i = L.first; i < L.first + L.count; ++i) {
-                const ConeItem& it = ex.items[i];
-                last_pass[it.xform] = std::max(last_pass[it.xform], L.pass);
-            }
         uint64_t a = 0;
         double alg = 0, mv = 0;
         for (const Launch& L : ex.launches) {
             alg += L.alg_bytes;
             mv += L.moved_bytes;
             if (L.pass == 0) a += L.cells;
-            for (uint32_t i = L.first; i < L.first + L.count; ++i) {
-                const ConeItem& it = ex.items[i];
-                const FfaXform& X = ex.xf[it.xform];
-                if (it.s1 <= it.s0 || it.s1 > it.node_size || it.node_start + it.node_size > X.m)
-                    throw std::runtime_error("schedule: tile outside its node");
-                if (it.mode == kModeTile) {
-                    const ConeNeed n = cone_need(it.node_size, it.s0, it.s1, it.levels, X.p);
-                    if (n.max_rows > kMaxRows || n.max_floats > kLdsDataFloats || n.ranges > kMaxRanges)
-                        throw std::runtime_error("schedule: tile exceeds the LDS budget");
-                } else if ((int)it.node_size * (int)X.p > kLdsDataFloats || it.node_size > (uint32_t)kMaxRows) {
-                    throw std::runtime_error("schedule: whole node exceeds the LDS budget");
-                }
-                // a launch's kernel instance stages enough register rows for every level
-                const int rw = L.rw ? (int)L.rw : merge_rows_per_wave((int)L.smax);
-                const int rows = it.mode == kModeTile
-                                     ? cone_need(it.node_size, it.s0, it.s1, it.levels, X.p).max_rows
-                                     : (int)it.node_size;
-                if (rows > kConeWaves * rw * row_pack((int)L.smax) || rows > lds_row_capacity(X.p, (int)L.smax))
-                    throw std::runtime_error("schedule: unit rows exceed its kernel instance's register rows");
-                if (L.pass == last_pass[it.xform]) {
-                    if (it.dst != kSelSnr || it.node_start != 0) throw std::runtime_error("schedule: bad final pass");
-                    covered[it.xform] += it.s1 - it.s0;
-                }
-            }
         }
-        for (size_t t = 0; t < ex.xf.size(); ++t)
-            if (covered[t] != ex.xf[t].m) throw std::runtime_error("schedule: final pass does not cover the transform");
         *transforms = ex.xf.size();
         *items = ex.items.size();
         *launches = ex.launches.size();
@@ -955,6 +961,22 @@ int rt_periodogram_device(const rt_plan* P, const float* d_data, size_t batch, s
     return guarded([&] {
         if (!batch || !P->pg.length) return RT_OK;
         run_periodogram(P, d_data, batch, data_stride, d_snrs, snr_stride, ws, ws_bytes, (hipStream_t)stream);
+        return RT_OK;
+    });
+}
+
+int rt_plan_check(const rt_plan* P, void* stream)
+{
+    return guarded([&] {
+        hipStream_t s = (hipStream_t)stream;
+        int flag = 0;
+        ck(hipMemcpyAsync(&flag, P->d_flag, sizeof flag, hipMemcpyDeviceToHost, s), "hipMemcpyAsync D2H");
+        ck(hipStreamSynchronize(s), "hipStreamSynchronize");
+        if (flag) {
+            ck(hipMemsetAsync(P->d_flag, 0, sizeof(int), s), "hipMemsetAsync");
+            ck(hipStreamSynchronize(s), "hipStreamSynchronize");
+            throw std::runtime_error("cone kernel: work item exceeded the LDS budget (S/N rows left unwritten)");
+        }
         return RT_OK;
     });
 }
@@ -1038,6 +1060,7 @@ int rt_profile_enable(int on)
 int rt_profile_reset(void)
 {
     return guarded([&] {
+        std::lock_guard<std::mutex> lk(g_prof.mu);
         for (auto& v : g_prof.rec)
             for (auto& r : v) {
                 g_prof.pool.push_back(r.a);
@@ -1053,6 +1076,7 @@ int rt_profile_read(int kind, double* ms, double* alg, double* moved, uint64_t* 
 {
     return guarded([&] {
         if (kind < 0 || kind > 1) throw std::invalid_argument("kind must be 0 or 1");
+        std::lock_guard<std::mutex> lk(g_prof.mu);
         double t = 0, b = 0, mv = 0;
         for (auto& r : g_prof.rec[kind]) {
             ck(hipEventSynchronize(r.b), "hipEventSynchronize");

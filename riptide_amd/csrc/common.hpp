@@ -144,13 +144,14 @@ constexpr uint64_t kTimelineCap = 1u << 21;
 // cone kernel feature bits (ConeArgs::flags)
 enum : uint32_t {
     kConeStoreFromRegs = 1u,   // non-final passes store the output level straight from registers
+    kConeFuse2 = 2u,           // two merge levels per LDS round trip where no level holds size-1 nodes
     kConeDiagNoSnr = 1u << 30, // diagnostics only (wrong results): skip the S/N epilogue
     kConeDiagNoMerge = 1u << 29, // diagnostics only (wrong results): skip the merge levels
     kConeDiagNoWrite = 1u << 28, // diagnostics only (wrong results): skip the level write-back
     kConeDiagNoBarrier = 1u << 27, // diagnostics only (wrong results): no barriers between merge levels
     kConeDiagNoLand = 1u << 26,  // diagnostics only (wrong results): fill loads issued but not landed in LDS
     kConeDiagNoDesc = 1u << 25,  // diagnostics only (wrong results): no descriptor table
-    kConeDefaultFeatures = 1u
+    kConeDefaultFeatures = 3u
 };
 enum : uint8_t { kSelLeaves = 0, kSelPing = 1, kSelPong = 2, kSelSnr = 3 };
 

@@ -624,6 +624,78 @@ __device__ __forceinline__ void merge_level_dense(const UnitMeta& M, const float
     }
 }
 
+// Two merge levels in one LDS round trip: the outputs of level l from the
+// rows of level l + 2 (the level l + 1 in between is never stored).  Output
+// row r of level l is H[h] + roll(T[t], sh) with H, T rows of level l + 1,
+// and H[h] = HH[hh] + roll(HT[ht], sH), T[t] = TH[th] + roll(TT[tt], sT) from
+// level l + 2, so bin j is
+//     (HH[hh][j] + HT[ht][(j + sH) mod p])
+//   + (TH[th][(j + sh) mod p] + TT[tt][(j + sh + sT) mod p])
+// -- the reference's float additions on the same operands in the same
+// association (transforms.hpp:13-27 applied twice), so bit-exact.  Per
+// 64-bin slot: 4 ds_read_b32 + 1 ds_write_b32 per two levels instead of 4 + 2.
+// Only levels whose nodes all have >= 2 rows (no carried size-1 nodes at
+// level l + 1) are fused.
+template <int SMAX, int RW>
+__device__ __forceinline__ void merge_level2_dense(const UnitMeta& M, const float* src, const uint32_t* desc,
+                                                   bool use_table, int p, int l, bool tile, int node_size, int lane,
+                                                   int wave, int nr, float (&v)[RW][SMAX])
+{
+    const int S = (p + 63) >> 6;
+    int o0 = 0, o1 = 0, o2 = 0, o3 = 0, s1 = 0, s2 = 0, s3 = 0;
+    if (lane < nr) {
+        const int r = wave + kConeWaves * lane;
+        uint32_t d0, dh, dt;
+        if (use_table) {
+            d0 = desc[desc_offset(M, l) + r];
+            const int b1 = desc_offset(M, l + 1);
+            dh = desc[b1 + (int)(d0 & 1023u)];
+            dt = desc[b1 + (int)((d0 >> 10) & 1023u)];
+        } else {
+            int h, t, sh;
+            row_desc(M, tile, node_size, l, r, p, h, t, sh);
+            d0 = pack_desc(h, t, sh);
+            row_desc(M, tile, node_size, l + 1, h, p, h, t, sh);
+            dh = pack_desc(h, t, sh);
+            row_desc(M, tile, node_size, l + 1, (int)((d0 >> 10) & 1023u), p, h, t, sh);
+            dt = pack_desc(h, t, sh);
+        }
+        const int sh = (int)(d0 >> 20), sH = (int)(dh >> 20), sT = (int)(dt >> 20);
+        int sTT = sh + sT;
+        sTT = sTT >= p ? sTT - p : sTT;
+        o0 = (int)(dh & 1023u) * p;
+        o1 = (int)((dh >> 10) & 1023u) * p + sH;
+        o2 = (int)(dt & 1023u) * p + sh;
+        o3 = (int)((dt >> 10) & 1023u) * p + sTT;
+        s1 = sH;
+        s2 = sh;
+        s3 = sTT;
+    }
+    const lds_cptr l1 = (lds_cptr)src + lane;
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+        const lds_cptr hrow = l1 + __builtin_amdgcn_readlane(o0, i);
+        lds_cptr b1 = l1 + __builtin_amdgcn_readlane(o1, i);
+        lds_cptr b2 = l1 + __builtin_amdgcn_readlane(o2, i);
+        lds_cptr b3 = l1 + __builtin_amdgcn_readlane(o3, i);
+        lds_cptr w1 = b1 - p, w2 = b2 - p, w3 = b3 - p;
+        asm("" : "+v"(b1), "+v"(w1), "+v"(b2), "+v"(w2), "+v"(b3), "+v"(w3));
+        const int ls1 = lane + __builtin_amdgcn_readlane(s1, i);
+        const int ls2 = lane + __builtin_amdgcn_readlane(s2, i);
+        const int ls3 = lane + __builtin_amdgcn_readlane(s3, i);
+#pragma unroll
+        for (int k = 0; k < SMAX; ++k) {
+            if (SMAX <= 5 || k < S) {
+                const int wk = p - 64 * k;
+                const float x1 = lds_ld((ls1 >= wk ? w1 : b1) + 64 * k);
+                const float x2 = lds_ld((ls2 >= wk ? w2 : b2) + 64 * k);
+                const float x3 = lds_ld((ls3 >= wk ? w3 : b3) + 64 * k);
+                v[i][k] = __fadd_rn(__fadd_rn(hrow[64 * k], x1), __fadd_rn(x2, x3));
+            }
+        }
+    }
+}
+
 // kPack2 variant (p <= 32): register row i of a wave holds two output rows,
 // the wave's row 2i in lanes 0-31 and row 2i + 1 in lanes 32-63 (bin j =
 // lane & 31), so a wave instruction does the work of two rows instead of
@@ -778,12 +850,18 @@ __device__ __forceinline__ void merge_levels(const UnitMeta& M, float* base, con
                                              __amdgpu_buffer_rsrc_t rs, uint32_t st_o0, uint32_t flags, float* dummy)
 {
     const int lane = tid & 63, wave = tid >> 6;
-    for (int l = L - 1; l >= 0; --l) {
-        const int orows = uni(M.nrows[l]);
+    // deepest first; two levels per step (merge_level2_dense) once no level
+    // below the step's output holds size-1 nodes, single steps before that
+    // and for a last odd level
+    const bool fuse = (flags & kConeFuse2) && SMAX != kPack2;
+    for (int l = L - 1; l >= 0;) {
+        // size-1 nodes exist at depth l only in whole units with node_size >> l < 2
+        const bool two = fuse && l >= 1 && (tile || (node_size >> l) >= 2);
+        const int lo = two ? l - 1 : l;          // output level of this step
+        const int orows = uni(M.nrows[lo]);
         const int nr = uni(orows > wave ? (orows - wave + kConeWaves - 1) / kConeWaves : 0);
         constexpr int S = slot_count(SMAX);
         float v[RW][S];
-        // size-1 nodes exist at depth l only in whole units with node_size >> l < 2
         const bool carried = !tile && (node_size >> l) < 2;
         if constexpr (SMAX == kPack2) {
             if (carried)
@@ -791,12 +869,15 @@ __device__ __forceinline__ void merge_levels(const UnitMeta& M, float* base, con
             else
                 merge_level_packed<RW, false>(M, base, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
         } else {
-            if (carried)
+            if (two)
+                merge_level2_dense<S, RW>(M, base, desc, use_table, p, lo, tile, node_size, lane, wave, nr, v);
+            else if (carried)
                 merge_level_dense<S, RW, true>(M, base, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
             else
                 merge_level_dense<S, RW, false>(M, base, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
         }
-        if (l == 0 && st) {
+        l = lo - 1;
+        if (lo == 0 && st) {
             if constexpr (SMAX == kPack2) store_rows_packed<RW>(v, p, lane, wave, nr, rs, st_o0);
             else store_rows<S, RW>(v, p, lane, wave, nr, rs, st_o0);
             return;

@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <cmath>
 #include <stdexcept>
+#include <string>
 
 namespace rt {
 
@@ -279,8 +280,12 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
 {
     out = ExecPlan();
     out.xf = xforms;
-    for (const FfaXform& X : xforms)
+    for (const FfaXform& X : xforms) {
         if (!merge_slots(X.p)) throw std::invalid_argument("phase bins too large for the LDS cone kernel");
+        if ((uint64_t)X.m * X.p * 4u >= kMaxBlockBytes)
+            throw std::invalid_argument("FFA transform block of " + std::to_string(X.m) + " x " + std::to_string(X.p) +
+                                        " floats exceeds the 2 GiB range of the cone kernel");
+    }
     const size_t nx = xforms.size();
     size_t g0 = 0;
     uint32_t group = 0;
@@ -386,6 +391,53 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
         g0 = g1;
         ++group;
     }
+    validate_exec_plan(out, snr_epilogue);
+}
+
+void validate_exec_plan(const ExecPlan& ex, bool snr_epilogue)
+{
+    std::vector<uint64_t> covered(ex.xf.size(), 0);
+    std::vector<uint32_t> last_pass(ex.xf.size(), 0);
+    for (const Launch& L : ex.launches)
+        for (uint32_t i = L.first; i < L.first + L.count; ++i)
+            last_pass[ex.items[i].xform] = std::max(last_pass[ex.items[i].xform], L.pass);
+    for (const FfaXform& X : ex.xf)
+        if ((uint64_t)X.m * X.p * 4u >= kMaxBlockBytes) throw std::runtime_error("schedule: transform block over 2 GiB");
+    for (const Launch& L : ex.launches) {
+        if (L.first + L.count > ex.items.size()) throw std::runtime_error("schedule: launch outside the item list");
+        for (uint32_t i = L.first; i < L.first + L.count; ++i) {
+            const ConeItem& it = ex.items[i];
+            if (it.xform >= ex.xf.size()) throw std::runtime_error("schedule: item of an unknown transform");
+            const FfaXform& X = ex.xf[it.xform];
+            if (merge_slots(X.p) != (int)L.smax) throw std::runtime_error("schedule: item in the wrong kernel variant");
+            if (it.s1 <= it.s0 || it.s1 > it.node_size || (uint64_t)it.node_start + it.node_size > X.m)
+                throw std::runtime_error("schedule: tile outside its node");
+            int rows;
+            if (it.mode == kModeTile) {
+                const ConeNeed n = cone_need(it.node_size, it.s0, it.s1, it.levels, X.p);
+                if (n.degenerate || n.max_rows > kMaxRows || n.max_floats > kLdsDataFloats || n.ranges > kMaxRanges ||
+                    it.levels > kMaxTileLevels)
+                    throw std::runtime_error("schedule: tile exceeds the LDS budget");
+                rows = n.max_rows;
+            } else {
+                if ((int)it.node_size * (int)X.p > kLdsDataFloats || it.node_size > (uint32_t)kMaxRows ||
+                    it.levels > kMaxLevels || (1u << it.levels) < it.node_size)
+                    throw std::runtime_error("schedule: whole node exceeds the LDS budget");
+                rows = (int)it.node_size;
+            }
+            // the launch's kernel instance stages enough register rows for every level
+            const int rw = L.rw ? (int)L.rw : merge_rows_per_wave((int)L.smax);
+            if (rows > kConeWaves * rw * row_pack((int)L.smax) || rows > lds_row_capacity(X.p, (int)L.smax))
+                throw std::runtime_error("schedule: unit rows exceed its kernel instance's register rows");
+            if (L.pass == last_pass[it.xform]) {
+                if (it.node_start != 0 || (snr_epilogue ? it.dst != kSelSnr : it.dst == kSelSnr))
+                    throw std::runtime_error("schedule: bad final pass");
+                covered[it.xform] += it.s1 - it.s0;
+            }
+        }
+    }
+    for (size_t t = 0; t < ex.xf.size(); ++t)
+        if (covered[t] != ex.xf[t].m) throw std::runtime_error("schedule: final pass does not cover the transform");
 }
 
 }  // namespace rt

@@ -74,6 +74,18 @@ struct ExecPlan {
 void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uint32_t num_widths,
                      uint64_t scratch_budget, ExecPlan& out);
 
+// Schedule invariants (every item fits its LDS / register budget and stays
+// inside its node, the final pass of every transform covers rows [0, m) once,
+// every transform block stays below the 2 GiB range of a 32-bit buffer
+// resource).  Throws std::runtime_error on a violation; build_exec_plan runs
+// it on every plan it returns, so a kernel never receives an invalid unit.
+void validate_exec_plan(const ExecPlan& ex, bool snr_epilogue);
+
+// Byte size limit of one transform block (m x p floats): the cone kernel
+// addresses a block through a buffer resource with a 32-bit byte count and
+// sends dropped lanes to offset 2^31.
+constexpr uint64_t kMaxBlockBytes = 1ull << 31;
+
 // Dependency-cone footprint of one tile (host mirror of the device range tree).
 struct ConeNeed { int max_rows = 0; int max_floats = 0; int ranges = 0; bool degenerate = false; };
 ConeNeed cone_need(uint32_t node_size, uint32_t s0, uint32_t s1, int levels, uint32_t p);

@@ -1,14 +1,17 @@
 """Multi-GPU DM-trial dispatcher: the replacement of rffa's CPU worker pool
 (riptide/pipeline/worker_pool.py:10-70) with the same contract: a list of DM
-trials in, the flat List[Peak] of every trial and search range out.
+trials in, the flat List[Peak] of every trial and search range out, in trial
+order and, within a trial, in range order (WorkerPool.process_fname_list,
+worker_pool.py:35-45, flattens its Pool.map results the same way).
 
 One process per GPU (torch.distributed, backend "nccl" = RCCL on ROCm, or
 "gloo" for CPU tests).  Trials are independent, so they are partitioned
 statically (round-robin by index) with no data-path collective; each rank
 batches its trials through the device-resident engine (dereddening +
 normalisation once per trial, then one periodogram per search range, exactly
-as WorkerPool.process_fname does), runs peak detection on the host, and the
-per-rank peak lists are gathered once at the end (KB-scale, latency-bound).
+as WorkerPool.process_fname does) and device peak detection, and the
+per-rank peak lists -- tagged with their trial index -- are gathered once at
+the end (KB-scale, latency-bound) and put back in trial order.
 """
 import logging
 import typing
@@ -22,7 +25,7 @@ log = logging.getLogger("riptide.dispatch")
 
 class Trial(typing.NamedTuple):
     """One dedispersed time series to search."""
-    data: np.ndarray          # float32 samples
+    data: np.ndarray          # samples as stored (float32, or uint8 / int8 8-bit data)
     tsamp: float
     metadata: dict            # must hold 'dm' (None allowed), like riptide Metadata
 
@@ -33,19 +36,32 @@ def shard(n_items, rank, world):
     return list(range(rank, n_items, world))
 
 
-class EngineSearcher:
-    """Batched GPU search of trials of one length: the hot path.  For every
-    search range: one compiled periodogram plan per (length, tsamp, range)
-    and device peak detection (riptide_amd.peaks.PeakFinder); only the peaks
-    leave the device."""
+def _group_by_shape(samples, tsamps):
+    """{(length, tsamp): [indices]} in first-seen order (device batches need
+    one series length and one sampling time)."""
+    groups = {}
+    for i, (x, ts) in enumerate(zip(samples, tsamps)):
+        groups.setdefault((int(np.asarray(x).size), float(ts)), []).append(i)
+    return groups
 
-    def __init__(self, deredden_params, range_confs, device=None, batch=8):
+
+class EngineSearcher:
+    """Batched GPU search of DM trials: the hot path.  For every search range:
+    one compiled periodogram plan per (length, tsamp, range) and device peak
+    detection (riptide_amd.peaks.PeakFinder); only the peaks leave the device.
+
+    Calling it on a list of Trial returns one peak list per trial, in the
+    order given (each in range order, as WorkerPool.process_fname)."""
+
+    def __init__(self, deredden_params, range_confs, device=None, batch=8, check=True):
         self.deredden_params = dict(deredden_params)
         self.range_confs = list(range_confs)
         self.device = device
         self.batch = int(batch)
+        self.check = bool(check)
         self._plans = {}
         self._finders = {}
+        self._ws = {}
 
     def _plan(self, n, tsamp, conf):
         from . import engine
@@ -65,6 +81,15 @@ class EngineSearcher:
             self._finders[key] = PeakFinder(plan, tobs, **kw)
         return self._finders[key]
 
+    def _workspace(self, plan, B):
+        import torch
+        need = plan.workspace_bytes(B)
+        ws = self._ws.get(id(plan))
+        if ws is None or ws.numel() < need:
+            ws = torch.empty(need, dtype=torch.uint8, device=plan.device)
+            self._ws[id(plan)] = ws
+        return ws
+
     def search_device(self, raw, tsamp, metadatas):
         """Peaks of every trial of a device batch raw [B, N] (float32): one
         list per trial, in range order (WorkerPool.process_fname)."""
@@ -76,39 +101,49 @@ class EngineSearcher:
         dms = [m.get("dm") for m in metadatas]
         for conf in self.range_confs:
             plan = self._plan(n, tsamp, conf)
-            snr = plan.run(x)
+            snr = plan.run(x, workspace=self._workspace(plan, B))
+            if self.check:
+                plan.check()          # device error flag: RuntimeError if a unit broke its budget
             for b, (peaks, _) in enumerate(self._finder(plan, n * tsamp, conf)(snr, dms=dms)):
                 out[b].extend(peaks)
         return out
 
+    def search_samples(self, samples, tsamps, metadatas):
+        """Per-trial peak lists of host sample arrays (float32 or 8-bit, as
+        stored): grouped by (length, tsamp), uploaded in device batches
+        (8-bit data converted on the device), results in input order."""
+        from .reading import upload_samples
+        per = [None] * len(samples)
+        for (n, tsamp), idx in _group_by_shape(samples, tsamps).items():
+            for b0 in range(0, len(idx), self.batch):
+                chunk = idx[b0:b0 + self.batch]
+                x = upload_samples([samples[i] for i in chunk], device=self.device)
+                for i, peaks in zip(chunk, self.search_device(x, tsamp, [metadatas[i] for i in chunk])):
+                    per[i] = peaks
+        return per
+
     def __call__(self, trials):
-        import torch
-        dev = torch.device("cuda", torch.cuda.current_device() if self.device is None else self.device)
-        peaks = []
-        groups = {}
-        for t in trials:
-            groups.setdefault((t.data.size, float(t.tsamp)), []).append(t)
-        for (n, tsamp), group in groups.items():
-            for b0 in range(0, len(group), self.batch):
-                chunk = group[b0:b0 + self.batch]
-                raw = torch.from_numpy(np.stack([np.asarray(t.data, np.float32) for t in chunk])).to(dev)
-                for found in self.search_device(raw, tsamp, [t.metadata for t in chunk]):
-                    peaks.extend(found)
-        return peaks
+        return self.search_samples([t.data for t in trials], [t.tsamp for t in trials],
+                                   [t.metadata for t in trials])
 
 
 def search_trials(trials, searcher, group=None):
     """Search this rank's share of `trials` with `searcher` (a callable taking
-    a list of Trial and returning List[Peak]); gather every rank's peaks.
-    Returns the full peak list on every rank, in trial order per rank."""
+    a list of Trial and returning one peak list per trial, in order); gather
+    every rank's lists.  Returns the full peak list on every rank, in trial
+    order (then range order within a trial): the WorkerPool contract."""
     import torch.distributed as dist
     distributed = dist.is_available() and dist.is_initialized()
     rank = dist.get_rank(group) if distributed else 0
     world = dist.get_world_size(group) if distributed else 1
-    mine = [trials[i] for i in shard(len(trials), rank, world)]
-    local = searcher(mine) if mine else []
-    if world == 1:
-        return list(local)
-    gathered = [None] * world
-    dist.all_gather_object(gathered, [tuple(p) for p in local], group=group)
-    return [Peak(*p) for part in gathered for p in part]
+    mine = shard(len(trials), rank, world)
+    local = searcher([trials[i] for i in mine]) if mine else []
+    if len(local) != len(mine):
+        raise RuntimeError("searcher must return one peak list per trial")
+    tagged = [(i, [tuple(p) for p in plist]) for i, plist in zip(mine, local)]
+    if world > 1:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, tagged, group=group)
+        tagged = [t for part in gathered for t in part]
+    tagged.sort(key=lambda t: t[0])
+    return [Peak(*p) for _, plist in tagged for p in plist]

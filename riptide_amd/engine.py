@@ -73,27 +73,46 @@ class PeriodogramPlan:
         return {"transforms": u[0].value, "items": u[1].value, "launches": u[2].value,
                 "alg_bytes": d[0].value, "moved_bytes": d[1].value, "cells": u[3].value}
 
-    def run(self, data, out=None, workspace=None, stream=None):
+    def run(self, data, out=None, workspace=None, stream=None, check=False):
         """S/N of a batch of series: data float32 [B, size] (or [size]) on the
-        device -> float32 [B, L, W].  Stream-ordered; no host synchronisation."""
+        device -> float32 [B, L, W].  Stream-ordered; no host synchronisation
+        unless `check` (then the plan's device error flag is read: see
+        check()).  Allocations happen on `stream` (default: the current one)."""
         import torch
         squeeze = data.dim() == 1
         if squeeze:
             data = data.unsqueeze(0)
-        if data.dtype != torch.float32 or data.device != self.device or data.shape[1] != self.size:
+        if data.dim() != 2 or data.dtype != torch.float32 or data.device != self.device or data.shape[1] != self.size:
             raise ValueError("data must be float32 [B, size] on the plan's device")
         if data.stride(1) != 1:
             raise ValueError("data rows must be contiguous")
         B = data.shape[0]
-        if out is None:
-            out = torch.empty((B, self.length, self.num_widths), dtype=torch.float32, device=self.device)
-        need = self.workspace_bytes(B)
-        if workspace is None or workspace.numel() < need:
-            workspace = torch.empty(need, dtype=torch.uint8, device=self.device)
-        _check(_L.rt_periodogram_device(self._h, _lib.ptr(data), B, data.stride(0), _lib.ptr(out),
-                                        self.length * self.num_widths, _lib.ptr(workspace), workspace.numel(),
-                                        _stream_handle(stream)))
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(s):
+            if out is None:
+                out = torch.empty((B, self.length, self.num_widths), dtype=torch.float32, device=self.device)
+            elif (out.dtype != torch.float32 or out.device != self.device or not out.is_contiguous()
+                  or tuple(out.shape) != (B, self.length, self.num_widths)):
+                raise ValueError(f"out must be a contiguous float32 [{B}, {self.length}, {self.num_widths}] "
+                                 "tensor on the plan's device")
+            need = self.workspace_bytes(B)
+            if workspace is None:
+                workspace = torch.empty(need, dtype=torch.uint8, device=self.device)
+            elif (workspace.dtype != torch.uint8 or workspace.device != self.device or not workspace.is_contiguous()
+                  or workspace.numel() < need):
+                raise ValueError(f"workspace must be a contiguous uint8 tensor of >= {need} bytes on the plan's device")
+            _check(_L.rt_periodogram_device(self._h, _lib.ptr(data), B, data.stride(0), _lib.ptr(out),
+                                            self.length * self.num_widths, _lib.ptr(workspace), workspace.numel(),
+                                            _stream_handle(s)))
+        if check:
+            self.check(s)
         return out[0] if squeeze else out
+
+    def check(self, stream=None):
+        """Raise EngineError if any cone work unit of the runs since the last
+        check broke its LDS / register budget (its S/N rows were left
+        unwritten).  Synchronises `stream` (default: the current stream)."""
+        _check(_L.rt_plan_check(self._h, _stream_handle(stream)))
 
     def __del__(self, _destroy=_L.rt_plan_destroy):
         # the default argument keeps the function alive through interpreter
@@ -118,16 +137,26 @@ def deredden_normalise(data, width_samples, min_points=101, deredden=True, norma
     squeeze = data.dim() == 1
     if squeeze:
         data = data.unsqueeze(0)
+    if data.dim() != 2 or data.dtype != torch.float32 or data.device.type != "cuda" or data.stride(1) != 1:
+        raise ValueError("data must be float32 [B, N] device rows with unit stride")
     B, N = data.shape
-    if out is None:
-        out = torch.empty_like(data)
-    need = deredden_workspace_bytes(N, width_samples, min_points, B)
-    if workspace is None or workspace.numel() < need:
-        workspace = torch.empty(need, dtype=torch.uint8, device=data.device)
-    _check(_L.rt_deredden_normalise_device(_lib.ptr(data), N, B, data.stride(0), int(width_samples),
-                                           int(min_points), int(bool(deredden)), int(bool(normalise)),
-                                           _lib.ptr(out), out.stride(0), _lib.ptr(workspace), workspace.numel(),
-                                           _stream_handle(stream)))
+    s = stream if stream is not None else torch.cuda.current_stream(data.device)
+    with torch.cuda.stream(s):
+        if out is None:
+            out = torch.empty((B, N), dtype=torch.float32, device=data.device)
+        elif (out.dim() != 2 or tuple(out.shape) != (B, N) or out.dtype != torch.float32
+              or out.device != data.device or out.stride(1) != 1):
+            raise ValueError("out must be float32 [B, N] rows with unit stride on the data's device")
+        need = deredden_workspace_bytes(N, width_samples, min_points, B)
+        if workspace is None:
+            workspace = torch.empty(need, dtype=torch.uint8, device=data.device)
+        elif (workspace.dtype != torch.uint8 or workspace.device != data.device or not workspace.is_contiguous()
+              or workspace.numel() < need):
+            raise ValueError(f"workspace must be a contiguous uint8 tensor of >= {need} bytes on the data's device")
+        _check(_L.rt_deredden_normalise_device(_lib.ptr(data), N, B, data.stride(0), int(width_samples),
+                                               int(min_points), int(bool(deredden)), int(bool(normalise)),
+                                               _lib.ptr(out), out.stride(0), _lib.ptr(workspace), workspace.numel(),
+                                               _stream_handle(s)))
     return out[0] if squeeze else out
 
 

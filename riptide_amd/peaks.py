@@ -120,7 +120,15 @@ class PeakFinder:
         return coeffs, polycos
 
     def __call__(self, snr, dms=None, stream=None):
-        """Peaks of every trial: list of (peaks sorted by S/N, polycos)."""
+        """Peaks of every trial: list of (peaks sorted by S/N, polycos).
+        Kernels, allocations and copies all run on `stream` (default: the
+        current stream)."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(snr.device)
+        with torch.cuda.stream(s):
+            return self._run(snr, dms, s)
+
+    def _run(self, snr, dms, stream):
         import torch
         from .engine import _stream_handle
         if snr.dim() == 2:

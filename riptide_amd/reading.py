@@ -318,32 +318,88 @@ def _raw_samples(fname, fmt, extra_keys=None):
     raise ValueError(f"unknown time series format {fmt!r}")
 
 
-def load_device_batch(fnames, fmt="sigproc", device=None, extra_keys=None, stream=None):
-    """Load time series files of equal length into one float32 [B, N] device
-    tensor: raw samples are copied to the device as stored (1 byte per sample
-    for 8-bit SIGPROC data) and converted there (rt_convert_samples_device,
-    bit-exact with numpy's astype(float32)).  Returns (tensor, [Metadata], tsamp)."""
+def upload_samples(raws, device=None, stream=None):
+    """Host sample arrays of equal length (float32, or uint8 / int8 8-bit data
+    as stored) -> one float32 [B, N] device tensor.  8-bit samples are copied
+    to the device as bytes (4x fewer bytes over PCIe than their float32
+    expansion) and converted there by rt_convert_samples_device, bit-exact
+    with numpy's astype(float32)."""
     import torch
     from . import _lib
     from .engine import _stream_handle
     dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+    n = int(raws[0].size)
+    if any(int(r.size) != n for r in raws):
+        raise ValueError("upload_samples needs series of equal length")
+    L = _lib.load()
+    kinds = {np.dtype(np.uint8): 0, np.dtype(np.int8): 1}
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    with torch.cuda.stream(s):
+        out = torch.empty((len(raws), n), dtype=torch.float32, device=dev)
+        for b, raw in enumerate(raws):
+            raw = np.ascontiguousarray(raw)
+            if raw.dtype == np.float32:
+                out[b].copy_(torch.from_numpy(raw))
+                continue
+            if raw.dtype not in kinds:
+                raise ValueError(f"unsupported sample type {raw.dtype}")
+            staged = torch.from_numpy(raw.view(np.uint8)).to(dev)
+            _lib.check(L.rt_convert_samples_device(_lib.ptr(staged), n, kinds[raw.dtype], _lib.ptr(out[b]),
+                                                   _stream_handle(s)))
+    return out
+
+
+def load_device_batch(fnames, fmt="sigproc", device=None, extra_keys=None, stream=None):
+    """Load time series files of equal length into one float32 [B, N] device
+    tensor (upload_samples).  Returns (tensor, [Metadata], tsamp)."""
     raws, metas, tsamps = [], [], []
     for fn in fnames:
         raw, meta, tsamp = _raw_samples(fn, fmt, extra_keys)
         raws.append(raw)
         metas.append(meta)
         tsamps.append(tsamp)
-    n = raws[0].size
-    if any(r.size != n for r in raws) or any(t != tsamps[0] for t in tsamps):
+    if any(t != tsamps[0] for t in tsamps):
         raise ValueError("load_device_batch needs files of equal length and sampling time")
-    out = torch.empty((len(raws), n), dtype=torch.float32, device=dev)
-    L = _lib.load()
-    kinds = {np.dtype(np.uint8): 0, np.dtype(np.int8): 1}
-    for b, raw in enumerate(raws):
-        if raw.dtype == np.float32:
-            out[b].copy_(torch.from_numpy(raw), non_blocking=False)
-            continue
-        staged = torch.from_numpy(raw.view(np.uint8)).to(dev)
-        _lib.check(L.rt_convert_samples_device(_lib.ptr(staged), n, kinds[raw.dtype], _lib.ptr(out[b]),
-                                               _stream_handle(stream)))
-    return out, metas, tsamps[0]
+    return upload_samples(raws, device=device, stream=stream), metas, tsamps[0]
+
+
+def write_presto(basename, data, tsamp, dm=0.0, mjd=60000.0, em_band="Radio"):
+    """Write a PRESTO .inf/.dat pair (float32 samples; used by tests, tools and
+    the cfg5 bench leg).  The .inf carries the keys inf2dict reads, one per
+    line, value after '=' at column 40, as PRESTO's own writer lays them out."""
+    data = np.ascontiguousarray(data, dtype=np.float32)
+    name = os.path.basename(basename)
+
+    def line(label, value):
+        return f" {label:<39s}=  {value}"
+
+    rows = [line("Data file name without suffix", name),
+            line("Telescope used", "Parkes"),
+            line("Instrument used", "Multibeam"),
+            line("Object being observed", "Fake"),
+            line("J2000 Right Ascension (hh:mm:ss.ssss)", "00:00:01.0000"),
+            line("J2000 Declination     (dd:mm:ss.ssss)", "-00:00:01.0000"),
+            line("Data observed by", "riptide_amd"),
+            line("Epoch of observation (MJD)", f"{mjd:.6f}"),
+            line("Barycentered?           (1=yes, 0=no)", "1"),
+            line("Number of bins in the time series", f"{data.size:d}"),
+            line("Width of each time series bin (sec)", f"{tsamp:.12e}"),
+            line("Any breaks in the data? (1=yes, 0=no)", "0"),
+            line("Type of observation (EM band)", em_band)]
+    if em_band == "Radio":
+        rows += [line("Beam diameter (arcsec)", "981"),
+                 line("Dispersion measure (cm-3 pc)", f"{dm:.12f}"),
+                 line("Central freq of low channel (Mhz)", "1182.1953125"),
+                 line("Total bandwidth (Mhz)", "400"),
+                 line("Number of channels", "1024"),
+                 line("Channel bandwidth (Mhz)", "0.390625"),
+                 line("Data analyzed by", "riptide_amd")]
+    else:
+        rows += [line("Field-of-view diameter (arcsec)", "100"),
+                 line("Central energy (kev)", "1.0"),
+                 line("Energy bandpass (kev)", "1.0"),
+                 line("Data analyzed by", "riptide_amd")]
+    with open(basename + ".inf", "w") as f:
+        f.write("\n".join(rows) + "\n")
+    data.tofile(basename + ".dat")
+    return basename + ".inf"

@@ -3,21 +3,36 @@ SURVEY.md §8 f2): same constructor arguments and the same
 `process_fname_list(fnames) -> List[Peak]` contract, so Pipeline.search
 (pipeline.py:177-189) can use it unchanged.
 
-Instead of one CPU process per DM trial, the files of a chunk are grouped by
-(length, sampling time) and searched in device batches: raw samples are
-loaded to the GPU (8-bit data converted there), dereddened and normalised
-once per trial (worker_pool.py:53-58), then every search range runs the FFA
-periodogram (one compiled plan per range and series shape) and device peak
-detection (riptide_amd.peaks).  Peaks come back per file in input order and,
-within a file, in range order -- the order WorkerPool.process_fname_list
-returns them in.
+Instead of one CPU process per DM trial, the files of a chunk are read once
+on the host (headers parsed, samples kept as stored), grouped by (length,
+sampling time) and searched in device batches: raw samples go to the GPU
+(8-bit data converted there), are dereddened and normalised once per trial
+(worker_pool.py:53-58), then every search range runs the FFA periodogram (one
+compiled plan per range and series shape) and device peak detection
+(riptide_amd.peaks).  Peaks come back per file in input order and, within a
+file, in range order -- the order WorkerPool.process_fname_list returns them
+in.
 """
 import logging
 
 from .dispatch import EngineSearcher
-from .reading import load_device_batch, _raw_samples
+from .reading import _raw_samples
 
 log = logging.getLogger("riptide.worker_pool")
+
+
+def iterate_chunks(fnames, chunksize=1):
+    """DMIterator.iterate_filenames (pipeline/dmiter.py:231-243) over an
+    already selected, DM-ordered file list: chunks of `chunksize`, the last
+    one possibly shorter."""
+    chunk = []
+    for fn in fnames:
+        chunk.append(fn)
+        if len(chunk) == chunksize:
+            yield chunk
+            chunk = []
+    if chunk:
+        yield chunk
 
 
 class GpuWorkerPool:
@@ -40,18 +55,13 @@ class GpuWorkerPool:
         return self.process_fname_list([fname])
 
     def process_fname_list(self, fnames):
-        fnames = list(fnames)
-        shapes = {}
-        for i, fn in enumerate(fnames):
+        raws, metas, tsamps = [], [], []
+        for fn in fnames:
             raw, meta, tsamp = _raw_samples(fn, self.fmt)
-            shapes.setdefault((raw.size, float(tsamp)), []).append(i)
-        per_file = [None] * len(fnames)
-        for (n, tsamp), idx in shapes.items():
-            for b0 in range(0, len(idx), self.batch):
-                chunk = idx[b0:b0 + self.batch]
-                x, metas, _ = load_device_batch([fnames[i] for i in chunk], self.fmt, device=self.searcher.device)
-                results = self.searcher.search_device(x, tsamp, metas)
-                for i, peaks in zip(chunk, results):
-                    per_file[i] = peaks
-                    log.debug(f"Done searching DM = {metas[chunk.index(i)].get('dm')}, peaks found: {len(peaks)}")
+            raws.append(raw)
+            metas.append(meta)
+            tsamps.append(tsamp)
+        per_file = self.searcher.search_samples(raws, tsamps, metas)
+        for meta, peaks in zip(metas, per_file):
+            log.debug(f"Done searching DM = {meta.get('dm')}, peaks found: {len(peaks)}")
         return [p for plist in per_file for p in plist]

@@ -127,3 +127,104 @@ def trial_input(k, n=1 << 22, tsamp=256e-6):
 def sample_rows(length, count=500, seed=123):
     count = min(count, length)
     return np.sort(np.random.RandomState(seed).choice(length, size=count, replace=False))
+
+
+# ---------------------------------------------------------------- end-to-end known answers
+# riptide/tests/presto_generation.py:31-58 + test_rseek.py:31-54: np.random.seed(0),
+# TimeSeries.generate(128 s, 256 us, P = 1 s, amplitude 20, ducy 0.02), PRESTO
+# format, rseek options Pmin 0.5, Pmax 2, bmin 480, bmax 520, smin 7 (others
+# at rseek's defaults: rmed_width 4, rmed_minpts 101, wtsp 1.5, clrad 0.2;
+# ffa_search(ducy_max=0.3)).
+RSEEK_CASE = dict(tobs=128.0, tsamp=256e-6, period=1.0, amplitude=20.0, ducy=0.02, dm=0.0,
+                  pmin=0.5, pmax=2.0, bmin=480, bmax=520, smin=7.0, rmed_width=4.0, rmed_minpts=101,
+                  wtsp=1.5, clrad=0.2, ducy_max=0.3)
+
+# riptide/tests/test_pipeline.py:39-74 with pipeline_config_A.yml: three DM
+# trials (dm, amplitude, ducy), each generated after np.random.seed(0).
+PIPELINE_CASE = dict(
+    tobs=128.0, tsamp=256e-6, period=1.0,
+    trials=[(0.0, 10.0, 0.05), (10.0, 20.0, 0.02), (20.0, 10.0, 0.05)],
+    dereddening={"rmed_width": 5.0, "rmed_minpts": 101},
+    ranges=[
+        {"name": "medium",
+         "ffa_search": {"period_min": 0.5, "period_max": 4.0, "bins_min": 480, "bins_max": 520, "fpmin": 8,
+                        "wtsp": 1.5},
+         "find_peaks": {"smin": 7.0}},
+        {"name": "long",
+         "ffa_search": {"period_min": 4.0, "period_max": 120.0, "bins_min": 960, "bins_max": 1040, "fpmin": 8,
+                        "wtsp": 1.5},
+         "find_peaks": {"smin": 7.0}},
+    ],
+    clustering_radius=0.2,
+)
+
+
+def generated_series(tobs, tsamp, period, amplitude, ducy, generate_signal):
+    """TimeSeries.generate (time_series.py:170-218) after np.random.seed(0),
+    as float32 (what presto_generation.py writes to the .dat file).
+    `generate_signal` is the implementation under test's (or the reference's)
+    libffa.generate_signal; numpy's legacy global RNG supplies the noise."""
+    np.random.seed(0)
+    nsamp = int(round(tobs / tsamp))
+    return np.asarray(generate_signal(nsamp, period / tsamp, phi0=0.5, ducy=ducy, amplitude=amplitude,
+                                      stdnoise=1.0), dtype=np.float32)
+
+
+# ---------------------------------------------------------------- cfg5: rffa beam of SIGPROC files
+# BASELINE.json configs[4] at reduced trial count: 2^23-sample SIGPROC .tim
+# DM trials @ 64 us (537 s, "SUPERB-like"), refdm = 10 k, searched with
+# riptide's example pipeline configuration (pipeline/config/example.yaml:
+# dereddening 5 s / 101 points; ranges short 0.2-0.5 s @ 240-260 bins, medium
+# 0.5-2 s @ 480-520, long 2-120 s @ 960-1040; smin 6).  Two top-hat pulsars
+# whose amplitude peaks at DM 40 (P = 0.7137 s) and DM 20 (P = 3.1416 s);
+# trials 6 and 7 are 8-bit files (unsigned / signed).
+CFG5 = dict(
+    n=1 << 23, tsamp=64e-6, nfiles=8,
+    dereddening={"rmed_width": 5.0, "rmed_minpts": 101},
+    ranges=[
+        {"name": "short",
+         "ffa_search": {"period_min": 0.2, "period_max": 0.5, "bins_min": 240, "bins_max": 260, "fpmin": 8,
+                        "wtsp": 1.5},
+         "find_peaks": {"smin": 6.0}},
+        {"name": "medium",
+         "ffa_search": {"period_min": 0.5, "period_max": 2.0, "bins_min": 480, "bins_max": 520, "fpmin": 8,
+                        "wtsp": 1.5},
+         "find_peaks": {"smin": 6.0}},
+        {"name": "long",
+         "ffa_search": {"period_min": 2.0, "period_max": 120.0, "bins_min": 960, "bins_max": 1040, "fpmin": 8,
+                        "wtsp": 1.5},
+         "find_peaks": {"smin": 6.0}},
+    ],
+    chunksize=4,
+)
+
+
+def cfg5_trial(k, n=None):
+    """(stored samples, SIGPROC header) of cfg5 DM trial k.  Stored dtype:
+    float32, or uint8 / int8 for trials 6 / 7 (what a reader hands over)."""
+    c = CFG5
+    n = c["n"] if n is None else n
+    tsamp = c["tsamp"]
+    dm = 10.0 * k
+    rs = np.random.RandomState(700 + k)
+    x = rs.normal(size=n)
+    walk = np.cumsum(rs.normal(size=n // 8192 + 1)) * 0.5
+    x = x + np.repeat(walk, 8192)[:n]
+    a1 = 30.0 * max(0.0, 1.0 - abs(dm - 40.0) / 25.0)
+    a2 = 22.0 * max(0.0, 1.0 - abs(dm - 20.0) / 25.0)
+    if a1:
+        x = x + tophat_train(n, tsamp, 0.7137, ducy=0.03, amplitude=a1)
+    if a2:
+        x = x + tophat_train(n, tsamp, 3.1416, ducy=0.02, amplitude=a2, phi0=0.6)
+    hdr = {"source_name": f"cfg5_DM{dm:.1f}", "tsamp": tsamp, "tstart": 60000.0, "src_raj": 123456.7,
+           "src_dej": -301502.5, "nchans": 1, "refdm": dm}
+    if k == 6:
+        data = np.clip(np.round(x * 10.0 + 128.0), 0, 255).astype(np.uint8)
+        hdr.update(nbits=8, signed=False)
+    elif k == 7:
+        data = np.clip(np.round(x * 10.0), -128, 127).astype(np.int8)
+        hdr.update(nbits=8, signed=True)
+    else:
+        data = x.astype(np.float32)
+        hdr.update(nbits=32)
+    return data, hdr

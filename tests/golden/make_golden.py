@@ -89,7 +89,34 @@ def ref_deredden_normalise(R, data, tsamp, rmed_width=4.0, rmed_minpts=101):
     return np.asarray((x - m) / v ** 0.5, dtype=np.float32)
 
 
+def transform_boundary_rows(n, tsamp, pmin, pmax, bmin, bmax):
+    """First and last evaluated row of every FFA transform: the plan of
+    periodogram.hpp:135-183 (rung ladder, bins loop, rows_eval via ceilshift)
+    restated to locate each transform's rows in the periodogram."""
+    import math
+    f0 = pmin / (tsamp * bmin)
+    g = (bmax + 1.0) / bmin
+    nds = int(math.ceil(math.log(pmax / pmin) / math.log(g)))
+    rows, row = [], 0
+    for ids in range(nds):
+        f = f0 * g ** ids
+        tau = f * tsamp
+        nd = int(math.floor(n / f))
+        pms = pmax / tau
+        bstop = min(bmax, nd, int(pms))
+        for b in range(bmin, bstop + 1):
+            m = nd // b
+            pceil = min(pms, b + 1.0)
+            ev = min(m, int(math.ceil(b * (m - 1.0) * (1.0 - b / pceil))))
+            if ev > 0:
+                rows += [row, row + ev - 1]
+            row += ev
+    return sorted(set(rows)), row
+
+
 def main():
+    if "--full-only" in sys.argv:
+        return main_full(load_reference())
     R = load_reference()
     lc = R.libcpp
     out = {}
@@ -170,8 +197,17 @@ def main():
         out[f"search_{name}_peaks"] = np.array([(p.ip, p.iw, p.snr) for p in peaks], dtype=np.float64).reshape(-1, 3)
 
     np.savez_compressed(os.path.join(HERE, "golden_small.npz"), **out)
+    main_full(R, meta)
 
-    # (vi) full-size BASELINE configs: digests, statistics, sampled rows, peaks
+
+def main_full(R, meta=None):
+    """(vi) full-size BASELINE configs: digests, per-width statistics, 5000
+    sampled rows plus the first and last evaluated row of every transform,
+    and the find_peaks list."""
+    if meta is None:
+        with open(os.path.join(HERE, "golden_full.json")) as f:
+            meta = json.load(f)["meta"]
+    lc = R.libcpp
     full = {"meta": meta, "configs": {}}
     for case in inputs.FULL_CASES:
         name = case["name"]
@@ -186,7 +222,10 @@ def main():
         pg = _Pgram(widths, periods, foldbins, snrs, raw.size * case["tsamp"], 0.0)
         peaks, _ = R.peak_detection.find_peaks(pg)
         t3 = time.time()
-        rows = inputs.sample_rows(periods.size)
+        bounds, total = transform_boundary_rows(case["n"], case["tsamp"], case["pmin"], case["pmax"],
+                                                case["bmin"], case["bmax"])
+        assert total == periods.size
+        rows = np.union1d(inputs.sample_rows(periods.size, count=5000), np.asarray(bounds, dtype=np.int64))
         full["configs"][name] = {
             "case": case,
             "input_sha": sha(raw),
@@ -198,6 +237,8 @@ def main():
             "snr_max": [float(v) for v in snrs.max(axis=0)],
             "snr_argmax": [int(v) for v in snrs.argmax(axis=0)],
             "snr_sum": [float(v) for v in snrs.astype(np.float64).sum(axis=0)],
+            "snr_abs_sum": [float(v) for v in np.abs(snrs.astype(np.float64)).sum(axis=0)],
+            "boundary_rows": [int(r) for r in bounds],
             "sample_rows": [int(r) for r in rows],
             "sample_snrs": snrs[rows].astype(float).tolist(),
             "peaks": [[int(p.ip), int(p.iw), float(p.snr)] for p in peaks],
@@ -205,7 +246,7 @@ def main():
         }
         print(f"full {name}: L={periods.size} peaks={len(peaks)} pgram={t2-t1:.2f}s peaks={t3-t2:.2f}s")
     with open(os.path.join(HERE, "golden_full.json"), "w") as f:
-        json.dump(full, f, indent=1)
+        json.dump(full, f, separators=(",", ":"))
 
 
 if __name__ == "__main__":

@@ -25,17 +25,18 @@ def make_trials():
 
 
 def oracle_searcher(trials):
+    """Searcher contract: one peak list per trial, in the order given."""
     from oracle import oracle as O
     from riptide_amd import Periodogram, find_peaks
-    peaks = []
+    out = []
     for t in trials:
         widths = O.generate_width_trials(CASE["bmin"], CASE["ducy_max"])
         periods, foldbins, snrs = O.periodogram(O.normalise(t.data), t.tsamp, widths, CASE["pmin"], CASE["pmax"],
                                                 CASE["bmin"], CASE["bmax"])
         meta = dict(t.metadata, tobs=t.data.size * t.tsamp)
         found, _ = find_peaks(Periodogram(widths, periods, foldbins, snrs, metadata=meta), smin=5.0)
-        peaks.extend(found)
-    return peaks
+        out.append(found)
+    return out
 
 
 def _worker(rank, world, port, q):
@@ -79,8 +80,22 @@ def test_gather_world2_matches_single():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    # every rank holds the full, identical list; as a set it equals the single-process run
+    # every rank holds the full, identical list, equal to the single-process
+    # run element by element: trial order, then range order (WorkerPool contract)
     assert results[0] == results[1]
-    key = lambda p: (p[7], p[5], p[4])   # (dm, ip, iw)
-    assert sorted(results[0], key=key) == sorted([tuple(p) for p in single], key=key)
-    assert {p[7] for p in results[0]} == {p.dm for p in single}
+    assert results[0] == [tuple(p) for p in single]
+    dms = [p.dm for p in single]
+    assert dms == sorted(dms)            # trials were given in DM order
+
+
+def test_search_trials_restores_trial_order():
+    """A searcher that groups trials (as EngineSearcher groups by shape) still
+    yields the peaks in trial order."""
+    from riptide_amd.dispatch import search_trials
+    from riptide_amd.peak_detection import Peak
+    trials = make_trials()
+
+    def fake(ts):
+        return [[Peak(1.0, 1.0, 1, 0.1, 0, k, 7.0, t.metadata["dm"])] for k, t in enumerate(ts)]
+    out = search_trials(trials, fake)
+    assert [p.dm for p in out] == [t.metadata["dm"] for t in trials]

@@ -298,11 +298,19 @@ def test_full_config(rt, golden_full, name):
     d = torch.from_numpy(raw).cuda()
     x = engine.deredden_normalise(d, int(round(4.0 / c["tsamp"])), 101)
     snrs = plan.run(x).cpu().numpy()
+    # >= 5000 sampled rows, including the first and last evaluated row of
+    # every FFA transform (tile / pass boundaries of the cone schedule)
     rows = np.asarray(g["sample_rows"])
+    assert rows.size >= 5000 and set(g["boundary_rows"]) <= set(g["sample_rows"])
     ok, msg = snr_close(snrs[rows], np.asarray(g["sample_snrs"], dtype=np.float32))
     assert ok, msg
     assert np.allclose(snrs.max(axis=0), g["snr_max"], rtol=1e-4)
     assert list(snrs.argmax(axis=0)) == g["snr_argmax"]
+    # every one of the L rows, per width, through its sum: |sum - ref| within
+    # 1e-4 relative of sum |S/N| (each row's own bound, summed)
+    s64 = snrs.astype(np.float64)
+    assert np.all(np.abs(s64.sum(axis=0) - np.asarray(g["snr_sum"])) <= 1e-4 * np.asarray(g["snr_abs_sum"]))
+    assert np.allclose(np.abs(s64).sum(axis=0), g["snr_abs_sum"], rtol=1e-5)
     pg = rt.Periodogram(plan.widths, periods, foldbins, snrs, metadata=rt.Metadata({"tobs": c["n"] * c["tsamp"],
                                                                                        "dm": 0.0}))
     peaks, _ = rt.find_peaks(pg)
@@ -383,41 +391,8 @@ def test_device_sample_conversion_exact(tmp_path):
         assert metas[0]["dm"] == 1.0
 
 
-def test_gpu_worker_pool_matches_per_file_search(rt, tmp_path):
-    from riptide_amd.reading import write_sigproc
-    from riptide_amd.worker_pool import GpuWorkerPool
-    n, tsamp = 1 << 16, 256e-6
-    fns = []
-    for k in range(5):
-        x = inputs.with_signal(n, tsamp, 300 + k, 0.37 + 0.02 * k, 18.0 if k % 2 == 0 else 0.0)
-        if k == 3:
-            x = np.clip(np.round(x * 20 + 128), 0, 255).astype(np.uint8)    # an 8-bit file in the mix
-            hdr = {"nbits": 8, "signed": False}
-        else:
-            hdr = {"nbits": 32}
-        fn = str(tmp_path / f"DM{k}.tim")
-        write_sigproc(fn, x, dict(hdr, tsamp=tsamp, nchans=1, refdm=float(k), tstart=58000.0, src_raj=0.0,
-                                  src_dej=0.0))
-        fns.append(fn)
-    dered = {"rmed_width": 1.0, "rmed_minpts": 101}
-    ranges = [{"ffa_search": {"period_min": 0.2, "period_max": 1.0, "bins_min": 100, "bins_max": 110},
-               "find_peaks": {"smin": 6.0}},
-              {"ffa_search": {"period_min": 1.0, "period_max": 2.5, "bins_min": 240, "bins_max": 260},
-               "find_peaks": {"smin": 6.0}}]
-    pool = GpuWorkerPool(dered, ranges, fmt="sigproc", batch=2)
-    got = pool.process_fname_list(fns)
-    # WorkerPool.process_fname, file by file (worker_pool.py:47-70)
-    ref = []
-    for fn in fns:
-        ts = rt.TimeSeries.from_sigproc(fn)
-        ts = ts.deredden(dered["rmed_width"], minpts=dered["rmed_minpts"]).normalise()
-        for conf in ranges:
-            kw = dict(conf["ffa_search"], deredden=False, already_normalised=True)
-            _, pg = rt.ffa_search(ts, **kw)
-            peaks, _ = rt.find_peaks(pg, **conf["find_peaks"])
-            ref.extend(peaks)
-    assert len(ref) > 0
-    assert got == ref
+# GpuWorkerPool is checked against reference-generated peak lists in
+# tests/test_gpu_e2e.py (cfg5 files, the rffa pipeline case).
 
 
 # ---------------------------------------------------------------- candidate folding

@@ -96,6 +96,20 @@ def test_schedule_cfg2_shape(lib):
     assert abs(u[3].value / 1e6 - 1331.6) < 0.1
 
 
+def test_schedule_refuses_blocks_over_2gib(lib):
+    """A transform block of >= 2^31 bytes would overflow the cone kernel's
+    32-bit buffer range: the planner refuses it with ValueError
+    text instead of producing silently wrong output.  f == 1 rung: m * p = N."""
+    u = [ctypes.c_uint64() for _ in range(4)]
+    d = [ctypes.c_double() for _ in range(2)]
+    args = (*(ctypes.byref(x) for x in u[:3]), ctypes.byref(d[0]), ctypes.byref(d[1]), ctypes.byref(u[3]))
+    n = (1 << 29) + 4096                       # 2^31 + 16 KiB of samples at the first rung
+    rc = lib.rt_schedule_check(n, 1e-3, 2, 0.24, 0.3, 240, 260, *args)
+    assert rc == 1 and b"2 GiB" in lib.rt_last_error()
+    n = (1 << 29) - 4096 * 260                 # every block below 2 GiB
+    assert lib.rt_schedule_check(n, 1e-3, 2, 0.24, 0.25, 240, 240, *args) == 0, lib.rt_last_error()
+
+
 def test_periodogram_length_errors(lib):
     from riptide_amd import _lib
     L = ctypes.c_size_t()

@@ -99,3 +99,43 @@ def test_presto_round_trip(tmp_path):
     assert d["barycentered"] is True and d["onoff_pairs"] == []
     with pytest.raises(ValueError):
         inf2dict(INF.replace("Parkes", "None (Artificial Data Set)"))
+
+
+# ---------------------------------------------------------------- the reference's own fixtures
+# riptide/tests/test_time_series.py:15-62 on riptide/tests/data/* (copied as
+# data under tests/golden/ref_data/): 16 samples 0..15 at 64 us in every file.
+REF_DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_data")
+
+
+def _check_fixture(ts):
+    assert ts.nsamp == 16
+    assert ts.tsamp == 64e-6
+    assert ts.data.dtype == np.float32
+    assert np.allclose(ts.data, np.arange(16))
+
+
+def test_reference_presto_fixtures():
+    from riptide_amd import TimeSeries
+    for name in ("fake_presto_radio.inf", "fake_presto_radio_breaks.inf"):
+        _check_fixture(TimeSeries.from_presto_inf(os.path.join(REF_DATA, name)))
+    with pytest.warns(UserWarning):
+        _check_fixture(TimeSeries.from_presto_inf(os.path.join(REF_DATA, "fake_presto_xray.inf")))
+    inf = PrestoInf(os.path.join(REF_DATA, "fake_presto_radio_breaks.inf"))
+    assert inf["breaks"] and len(inf["onoff_pairs"]) > 0
+
+
+def test_reference_sigproc_fixtures():
+    from riptide_amd import TimeSeries
+    for name in ("fake_sigproc_float32.tim", "fake_sigproc_uint8.tim", "fake_sigproc_int8.tim"):
+        _check_fixture(TimeSeries.from_sigproc(os.path.join(REF_DATA, name)))
+    with pytest.raises(ValueError):
+        TimeSeries.from_sigproc(os.path.join(REF_DATA, "fake_sigproc_uint8_nosignedkey.tim"))
+
+
+def test_presto_writer_round_trip(tmp_path):
+    from riptide_amd.reading import write_presto
+    x = np.random.RandomState(3).normal(size=777).astype(np.float32)
+    fn = write_presto(str(tmp_path / "p"), x, 2.56e-4, dm=12.5)
+    data, meta, tsamp = read_presto(fn)
+    assert np.array_equal(data, x) and tsamp == 2.56e-4 and meta["dm"] == 12.5
+    assert meta["tobs"] == 777 * 2.56e-4

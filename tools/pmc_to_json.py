@@ -32,10 +32,13 @@ def main():
     write = sums["WRITE_SIZE"] * 1024.0
     launches = len(disp["FETCH_SIZE"])
     commit = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import source_digest
     res = {
         "kernel": "cone_kernel",
         "source": root,
         "commit": commit,
+        "csrc_sha": source_digest(),      # bench.py uses the summary only for these exact kernel sources
         "trials": trials,
         "launches": launches,
         "fetch_bytes_per_trial": fetch / trials,
