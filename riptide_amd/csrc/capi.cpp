@@ -156,10 +156,12 @@ struct Profiler {
 struct DevicePlan {
     ExecPlan ex;
     UnitDesc* d_units = nullptr;
+    uint32_t* d_blob = nullptr;     // tile-unit metadata (build_tile_blob)
     int device = 0;
     ~DevicePlan()
     {
         if (d_units) (void)hipFree(d_units);
+        if (d_blob) (void)hipFree(d_blob);
     }
     void upload()
     {
@@ -184,18 +186,24 @@ struct DevicePlan {
             d.mode = it.mode;
             d.src = it.src;
             d.dst = it.dst;
+            d.pad = it.pad;
             u[i] = d;
         }
         // Test hook (RIPTIDE_AMD_DEBUG_CORRUPT_UNIT=1): give the first whole-node
-        // unit 4096 rows after the host validation, so the kernel's own budget
-        // check refuses it and sets the error flag (exercises rt_plan_check).
+        // unit more merge levels than any kernel instance runs, after the host
+        // validation, so the kernel's own check refuses it and sets the error
+        // flag (exercises rt_plan_check).
         if (const char* e = std::getenv("RIPTIDE_AMD_DEBUG_CORRUPT_UNIT"))
             if (std::atoi(e) != 0)
                 for (UnitDesc& d : u)
                     if (d.mode == kModeWhole) {
-                        d.node_size = 4096;
+                        d.levels = kMaxLevels + 1;
                         break;
                     }
+        ck(hipMalloc(&d_blob, std::max<size_t>(4, ex.blob.size()) * sizeof(uint32_t)), "hipMalloc");
+        if (!ex.blob.empty())
+            ck(hipMemcpy(d_blob, ex.blob.data(), ex.blob.size() * sizeof(uint32_t), hipMemcpyHostToDevice),
+               "upload blob");
         ck(hipMalloc(&d_units, std::max<size_t>(1, u.size()) * sizeof(UnitDesc)), "hipMalloc");
         if (!u.empty())
             ck(hipMemcpy(d_units, u.data(), u.size() * sizeof(UnitDesc), hipMemcpyHostToDevice), "upload units");
@@ -212,6 +220,7 @@ void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStrea
     a.batch = batch;
     a.flags = kConeDefaultFeatures;
     if (const char* e = std::getenv("RIPTIDE_AMD_CONE_FLAGS")) a.flags = (uint32_t)std::strtoul(e, nullptr, 0);
+    a.blob = P.d_blob;
     for (size_t li = 0; li < P.ex.launches.size(); ++li) {
         const Launch& L = P.ex.launches[li];
         a.items = P.d_units + L.first;

@@ -27,37 +27,48 @@
 
 namespace rt {
 
-// ---- cone kernel geometry (gfx950: 160 KiB LDS per CU).  512-thread
-// workgroups; RT_CONE_WGS = 2: ~77 KiB of LDS each, two per CU; RT_CONE_WGS =
-// 1: one ~155 KiB workgroup per CU (twice the rows per unit, so fewer HBM
-// passes, 256 VGPRs per lane).  The level buffer holds dense rows (stride p).
-#ifndef RT_CONE_BLOCK
-#define RT_CONE_BLOCK 512
+// ---- cone kernel geometry (gfx950: 160 KiB LDS per CU).  Two layouts
+// (RT_CONE_BUFFERS):
+//   2: one persistent 1024-thread workgroup per CU (16 waves, <= 128 VGPRs)
+//      with two 70 KiB level buffers: it merges one unit in one buffer while
+//      the next unit's bottom level streams into the other by LDS DMA;
+//   1: two 512-thread workgroups per CU (8 waves each, <= 128 VGPRs), one
+//      71 KiB level buffer each: a unit's DMA is waited for at its start and
+//      the CU's other workgroup fills that wait.
+// The merged levels are dense rows (stride p).
+#ifndef RT_CONE_BUFFERS
+#define RT_CONE_BUFFERS 1
 #endif
-#ifndef RT_CONE_WGS
-#define RT_CONE_WGS 2
-#endif
-constexpr int kConeWgsPerCu = RT_CONE_WGS;
-static_assert(kConeWgsPerCu >= 1 && kConeWgsPerCu <= 3, "RT_CONE_WGS is 1, 2 or 3");
-constexpr int kConeBlock = RT_CONE_BLOCK;   // 8 waves; two workgroups per CU (RT_CONE_BLOCK=1024: 16 waves, 64 VGPRs, measured slower)
+constexpr int kConeBuffers = RT_CONE_BUFFERS;
+static_assert(kConeBuffers == 1 || kConeBuffers == 2, "RT_CONE_BUFFERS is 1 or 2");
+constexpr int kConeWgsPerCu = kConeBuffers == 2 ? 1 : 2;
+constexpr int kConeBlock = kConeBuffers == 2 ? 1024 : 512;
 constexpr int kConeWaves = kConeBlock / 64;
 constexpr int kConeWavesPerSimd = kConeWgsPerCu * kConeWaves / 4;
-constexpr int kLdsDataFloats = kConeWgsPerCu == 1 ? 36864 : (kConeWgsPerCu == 2 ? 17408 : 11264);   // 144 | 68 | 44 KiB level buffer
+constexpr int kLdsBufFloats = kConeBuffers == 2 ? 17920 : 18176;   // one level buffer: a unit's fill (16-byte chunks, runs per range)
+constexpr int kLdsDataFloats = kLdsBufFloats - 256;   // rows x p of any level (the rest: per-range 16-byte phase slack)
 constexpr int kLdsPadFloats = 128;          // slack read (never used) by the unused slots of the last row
-constexpr int kMaxRows = 512;               // rows per level (source-row table, descriptors)
-constexpr int kDescEntries = kConeWgsPerCu == 1 ? 2048 : (kConeWgsPerCu == 2 ? 1024 : 768);   // row-descriptor table (all levels of a unit)
+constexpr int kMaxRows = 384;               // rows per level (row-offset table, descriptors)
+constexpr int kDescEntries = 1024;          // row-descriptor table (all levels of a unit)
 constexpr int kMaxTileLevels = 6;           // L for tile items
 constexpr int kMaxLevels = 11;              // merge levels of any unit (whole units: ceil(log2(kMaxRows)))
 constexpr int kMaxRanges = (1 << (kMaxTileLevels + 1)) - 1;
 constexpr int kMaxWidths = 32;              // boxcar widths handled by the fused S/N epilogue
 constexpr int kSnrChunk = 17;               // S/N epilogue: columns per lane held in registers
-constexpr int kStageRegs = kConeBlock >= 1024 || kConeWgsPerCu == 3 ? 25 : (kConeWgsPerCu == 1 ? 96 : 45);   // merge: staged values per lane (rows x slots)
+constexpr int kStageRegs = kConeBuffers == 2 ? 25 : 45;   // merge: staged values per lane (rows x slots)
 constexpr int kMaxSlots = 45;               // merge: 64-bin slots per row (p <= 2880)
-constexpr int kMaxRowsPerWave = kConeBlock >= 1024 || kConeWgsPerCu == 3 ? 12 : (kConeWgsPerCu == 1 ? 48 : 24);   // merge: staged rows per wave
-// float4 chunks per thread of the fill: a level of n rows spans at most
-// n*p/4 + n aligned chunks (one extra per row for misalignment), n*p <=
-// kLdsDataFloats and n <= kMaxRows.
-constexpr int kFillChunks = (kLdsDataFloats / 4 + kMaxRows + kConeBlock - 1) / kConeBlock;
+constexpr int kMaxRowsPerWave = 24;         // merge: staged rows per wave
+// header words of a unit's host-built blob (plan.hpp build_tile_blob); a
+// unit without one (a whole unit too large for the descriptor table) has
+// UnitDesc::pad = kNoBlob.  kCarriedRow: the tail-row field of a size-1 node
+// carried unchanged.
+constexpr int kBlobHeader = 32;
+constexpr uint32_t kNoBlob = 0xFFFFFFFFu;
+constexpr uint32_t kCarriedRow = 1023;
+// 16-byte chunks of a unit's LDS DMA fill (setup_unit): a whole unit's block
+// of n*p floats at 16-byte phase <= 3, or a tile's ranges, each a run at its
+// own phase (<= 2^L runs); the planner keeps every unit within a buffer.
+RT_HD inline int fill_chunks_bound(int n, int p, int runs) { return (n * p + 6 * runs + 3) >> 2; }
 
 // Merge variant for rows of p phase bins: slots per row rounded up to an
 // instantiated width (1..5, 8, 16, 45), or kPack2 for p <= 32 (two rows per
@@ -85,8 +96,11 @@ RT_HD constexpr int row_pack(int smax) { return smax == kPack2 ? 2 : 1; }
 
 // Register rows per wave the merge stages for a variant (register budget);
 // each register row holds row_pack(smax) output rows.
+// register rows per wave of the 4-slot variant: its LDS capacity at p >= 221
+// (5 x 16 waves = 80 >= 17664 / 221) or at p >= 240 (9 x 8 waves = 72 >=
+// 16128 / 240)
 #ifndef RT_RW4
-#define RT_RW4 9   // register rows per wave of the 4-slot variant: 9 x 8 waves = 72 rows = its LDS capacity at p >= 242 (the register budget would allow 11; the 2 extra register rows would be computed and dropped on every level)
+#define RT_RW4 (kConeBuffers == 2 ? 5 : 9)
 #endif
 RT_HD constexpr int merge_rows_per_wave(int smax)
 {
@@ -177,7 +191,7 @@ struct UnitDesc {
     float stdnoise;
     uint64_t src_off, buf_off, snr_row;
     uint8_t levels, mode, src, dst;
-    uint32_t pad;
+    uint32_t pad;         // tile units: word offset of the unit's blob in ConeArgs::blob
 };
 static_assert(sizeof(UnitDesc) == 64, "UnitDesc layout");
 
@@ -195,6 +209,7 @@ struct ConeArgs {
     uint64_t snr_stride;
     const uint32_t* widths;  // boxcar widths (bins), device array of num_widths
     int* error_flag;      // set non-zero if a work item violates the LDS budget
+    const uint32_t* blob; // host-built tile-unit metadata (plan.hpp build_tile_blob); UnitDesc::pad = word offset
     unsigned long long* stamps;   // RT_STAMPS diagnostic builds only: per-phase cycles
     uint32_t batch;       // trials: work unit u = (item u / batch, trial u % batch)
     uint32_t flags;       // kCone* feature bits (A/B experiments; default all set)

@@ -8,6 +8,8 @@
 // bit-identical to the strict restatement of downsample.hpp:44-82.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -157,35 +159,27 @@ hipError_t launch_downsample_ladder(const float* x, uint64_t n_in, uint64_t x_st
 // ---------------------------------------------------------------------------
 // Cone kernel
 // ---------------------------------------------------------------------------
-// One workgroup (512 threads, 77 KiB of LDS: two workgroups per CU) per work
-// unit = one work item (UnitDesc) of one trial: `levels` merge levels of the
-// FFA recursion for the rows of one tile (or one whole node), held in LDS.
-// Phases:
-//   1. setup: unit view, rows per level, range tree of tile units (the
-//      planner guarantees 2^l ranges at cone level l)
-//   2. fill of the bottom level (dense rows, stride p): 16-byte buffer loads
-//      into registers; while they are in flight, the row descriptors of
-//      every level are built into a table; then landed in LDS
-//   3. merge levels, deepest first (transforms.hpp:13-27), one row per wave
-//      and one phase bin per lane:
+// A work unit = one work item (UnitDesc) of one trial: `levels` merge levels
+// of the FFA recursion for the rows of one tile (or one whole node), in LDS.
+//   1. begin: the unit's view (one scalar load of its UnitDesc); the bottom
+//      level is LDS-DMA'd from the transform block (a whole unit: one run of
+//      16-byte chunks; a tile unit: one run per range of its dependency cone,
+//      listed in the host-built blob, which is DMA'd alongside: rows per
+//      level, the row-descriptor table of every level, the bottom rows' LDS
+//      offsets -- build_tile_blob, plan.cpp)
+//   2. merge levels, deepest first (transforms.hpp:13-27), one row per wave
+//      and one phase bin per lane, two levels per LDS round trip where no
+//      level holds size-1 nodes:
 //          out[r][j] = H[h(r)][j] + T[t(r)][(j + shift(r)) mod p]
-//      Lane i unpacks the descriptor of the wave's i-th row into LDS offsets;
+//      Lane i holds the descriptor of the wave's i-th row as LDS offsets;
 //      the row loop takes them with v_readlane.  Bins j = lane + 64k use
-//      immediate offsets, so a 64-bin slot is one ds_read for H, one for T
-//      (consecutive lanes -> consecutive banks) and one ds_write.  A level's
+//      immediate offsets, so a 64-bin slot is one ds_read per operand
+//      (consecutive lanes -> consecutive banks) and one ds_write.  A step's
 //      outputs are staged in registers between two barriers (in place).
-//   4. a non-final pass stores its last level straight from the registers;
+//   3. a non-final pass stores its last level straight from the registers;
 //      a final pass runs the fused boxcar S/N epilogue (snr.hpp:37-65) on it.
-// The other workgroup on the CU overlaps its latency-bound phases (setup,
-// fill wait) with this one's LDS and VALU work; the kernel as a whole is
-// bound by the CU's LDS, VALU and scalar issue.
-struct Range {          // rows [lo, hi] of one node of the split tree
-    int size;           // rows of the node
-    int lo, hi;         // node-local rows
-    int start;          // first row of the node within the transform
-    int base;           // first LDS row of this range in its level's packed layout
-};
-
+// Whole units compute their descriptors on the fly (node partition
+// arithmetic, no table).
 
 // LDS-only workgroup barrier: orders LDS accesses without waiting for the
 // global loads or stores that are still in flight.
@@ -211,16 +205,6 @@ __device__ __forceinline__ T* uni_ptr(T* p)
     return reinterpret_cast<T*>(uni64(reinterpret_cast<uint64_t>(p)));
 }
 
-__device__ __forceinline__ int wave_incl_scan_int(int v, int lane)
-{
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(v, o, 64);
-        if (lane >= o) v += y;
-    }
-    return v;
-}
-
 // Wave-uniform view of one unit (scalar registers).
 struct UnitView {
     int item, trial;
@@ -228,48 +212,24 @@ struct UnitView {
     int p, m, rows_eval;
     uint64_t src_off, buf_off, snr_row;
     float stdnoise;
+    uint32_t blob;            // tile units: word offset of the host-built blob
 };
 
-// Per-unit metadata in LDS (double-buffered): the unit's view, rows per level
-// and the range tree of tile units.  Everything the merge and the epilogue of
-// a unit need is read from here, never from global memory, so no vmcnt wait
-// (which would also wait for the next unit's DMA) is needed after setup.
-struct UnitMeta {
-    UnitView view;
-    int nrows[kMaxLevels + 1];       // rows of every level (0 = output level)
-    int doff[kMaxLevels + 1];        // first descriptor-table entry of every level
-    Range ranges[kMaxRanges];        // tile units: level l holds 2^l ranges at (1 << l) - 1
-};
-
-__device__ __forceinline__ UnitView read_view(const UnitMeta& M)
-{
-    UnitView v;
-    v.item = uni(M.view.item);
-    v.trial = uni(M.view.trial);
-    v.node_start = uni(M.view.node_start);
-    v.node_size = uni(M.view.node_size);
-    v.s0 = uni(M.view.s0);
-    v.s1 = uni(M.view.s1);
-    v.levels = uni(M.view.levels);
-    v.mode = uni(M.view.mode);
-    v.src = uni(M.view.src);
-    v.dst = uni(M.view.dst);
-    v.p = uni(M.view.p);
-    v.m = uni(M.view.m);
-    v.rows_eval = uni(M.view.rows_eval);
-    v.src_off = uni64(M.view.src_off);
-    v.buf_off = uni64(M.view.buf_off);
-    v.snr_row = uni64(M.view.snr_row);
-    v.stdnoise = __int_as_float(uni(__float_as_int(M.view.stdnoise)));
-    return v;
-}
+typedef const __attribute__((address_space(4))) uint32_t* const_u32_ptr;
 
 __device__ __forceinline__ UnitView unit_view(const ConeArgs& a, int item, int trial)
 {
     UnitView v;
     v.item = uni(item);
     v.trial = uni(trial);
-    const UnitDesc d = a.items[v.item];
+    // constant address space: scalar (SMEM) loads, counted in lgkmcnt, so
+    // they never wait behind the vector-memory queue (DMA fills, stores)
+    const const_u32_ptr w = (const_u32_ptr)(uintptr_t)(a.items + v.item);
+    uint32_t x[sizeof(UnitDesc) / 4];
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(UnitDesc) / 4); ++i) x[i] = w[i];
+    UnitDesc d;
+    __builtin_memcpy(&d, x, sizeof d);
     v.node_start = uni((int)d.node_start);
     v.node_size = uni((int)d.node_size);
     v.s0 = uni((int)d.s0);
@@ -285,73 +245,29 @@ __device__ __forceinline__ UnitView unit_view(const ConeArgs& a, int item, int t
     v.buf_off = uni64(d.buf_off);
     v.snr_row = uni64(d.snr_row);
     v.stdnoise = __int_as_float(uni(__float_as_int(d.stdnoise)));
+    v.blob = (uint32_t)uni((int)d.pad);
     return v;
 }
 
-// Metadata of unit u into M (+ the source-row table of its bottom level).
-// Every thread calls it; it ends with a barrier.
-__device__ __forceinline__ void setup_unit(const ConeArgs& a, int item, int trial, UnitMeta& M, int* src_row, int tid)
+// Per-unit context (wave-uniform) and its LDS metadata: for tile units the
+// blob (kBlobHeader words of header, the DMA runs, the descriptor table, the
+// bottom-row offsets) DMA'd into `aux`.
+constexpr int kAuxWords = kBlobHeader + 4 * (1 << kMaxTileLevels) + kDescEntries + kMaxRows;
+struct UnitCtx {
+    UnitView U;
+    bool tile;                // a tile unit (else: a whole node)
+    bool table;               // the host-built blob is in aux (every tile unit, most whole units)
+    int al;                   // whole units: 16-byte phase (floats) of the block
+    int nruns, entries, nb;   // tile units: header words 24..26
+    const uint32_t* aux;      // tile units: the blob in LDS
+};
+
+__device__ __forceinline__ int rows_at(const UnitCtx& C, int l) { return C.table ? uni((int)C.aux[l]) : C.U.node_size; }
+__device__ __forceinline__ int desc_offset(const UnitCtx& C, int l) { return uni((int)C.aux[12 + l]); }
+__device__ __forceinline__ const uint32_t* desc_table(const UnitCtx& C) { return C.aux + kBlobHeader + 4 * C.nruns; }
+__device__ __forceinline__ const int* bottom_offsets(const UnitCtx& C)
 {
-    const int lane = tid & 63, wave = tid >> 6;
-    const UnitView U = unit_view(a, item, trial);
-    if (tid == 0) M.view = U;
-    const int L = U.levels;
-    if (U.mode == kModeTile) {
-        // level l (wave l): lane i walks the head/tail path i (MSB first) from
-        // the tile; the planner guarantees every node above the bottom level
-        // has >= 2 rows, so level l has exactly 2^l ranges
-        if (wave <= L) {
-            const int l = wave;
-            const int nr = 1 << l;
-            Range R{0, 0, -1, 0, 0};
-            if (lane < nr) {
-                uint32_t size = (uint32_t)U.node_size, lo = (uint32_t)U.s0, hi = (uint32_t)U.s1 - 1;
-                int start = U.node_start;
-                for (int d = 0; d < l; ++d) {
-                    const uint32_t sh = size >> 1, st = size - sh;
-                    const bool tail = (lane >> (l - 1 - d)) & 1;
-                    const uint32_t cs = tail ? st : sh;
-                    const float k = merge_coef(cs, size);
-                    lo = merge_index(k, lo);
-                    hi = merge_index(k, hi);
-                    if (tail) start += (int)sh;
-                    size = cs;
-                }
-                R.size = (int)size;
-                R.lo = (int)lo;
-                R.hi = (int)hi;
-                R.start = start;
-            }
-            const int c = R.hi - R.lo + 1;
-            const int incl = wave_incl_scan_int(lane < nr ? c : 0, lane);
-            if (lane < nr) {
-                R.base = incl - c;
-                M.ranges[nr - 1 + lane] = R;
-            }
-            if (lane == 63) M.nrows[l] = incl;
-        }
-        lds_barrier();
-        if (tid == 0) {
-            int o = 0;
-            for (int l = 0; l <= L; ++l) {
-                M.doff[l] = o;
-                o += M.nrows[l];
-            }
-        }
-        const int nb = uni(M.nrows[L]);
-        const Range* lv = &M.ranges[(1 << L) - 1];
-        for (int r = tid; r < nb; r += kConeBlock) {
-            int lo = 0;
-            for (int step = (1 << L) >> 1; step > 0; step >>= 1)
-                if (lv[lo + step].base <= r) lo += step;
-            const Range R = lv[lo];
-            src_row[r] = R.start + R.lo + (r - R.base);
-        }
-    } else if (tid <= L) {
-        M.nrows[tid] = U.node_size;
-        M.doff[tid] = tid * U.node_size;
-    }
-    lds_barrier();
+    return reinterpret_cast<const int*>(desc_table(C) + C.entries);
 }
 
 // Raw buffer resource over `bytes` bytes at p (gfx9 dword3: 32-bit data
@@ -361,109 +277,80 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* p, uin
     return __builtin_amdgcn_make_buffer_rsrc(uni_ptr(const_cast<void*>(p)), (short)0, uni((int)bytes), 0x00020000);
 }
 
-// Fill of a unit's bottom level into dense rows (stride p): 16-byte aligned
-// global loads into registers
-// (issued before the descriptor build, so their latency overlaps it), then
-// landed in LDS.  A whole unit is
-// one contiguous block of rows; a tile unit is read row by row (its rows come
-// from 2^L separate ranges).  Chunk k of a thread holds elements
-// e[k] .. e[k] + 3 of the LDS segment starting at lo[k]; elements outside
-// [0, len) are dropped.
-struct Fill {
-    float4 v[kFillChunks];
-    int lo[kFillChunks], e[kFillChunks];
-    int len;
-    int al;             // whole units: the level buffer starts at data + al (LDS 16-B phase = global phase)
-};
-
-__device__ __forceinline__ void fill_issue(const ConeArgs& a, const UnitMeta& M, const UnitView& U,
-                                           const int* src_row, int tid, Fill& F)
+// LDS DMA of `nch` 16-byte chunks from byte offset `goff` of resource rs
+// into lds[0 .. 4 nch) (floats), by the waves `wave0 .. W - 1` of the
+// workgroup in steps of `wstep` waves: a wave instruction moves 64
+// consecutive chunks (destination M0 + 16 lane); lanes past the end are
+// exec-masked off and write nothing.
+__device__ __forceinline__ void dma_run(__amdgpu_buffer_rsrc_t rs, uint32_t goff, int nch, float* lds, int wave,
+                                        int wstep, int lane)
 {
+    for (int c0 = wave * 64; c0 < nch; c0 += wstep * 64) {
+        const int c = c0 + lane;
+        if (c < nch)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds + 4 * c0), 16,
+                                                     (int)(goff + 16u * (uint32_t)c), 0, 0, 0);
+    }
+}
+
+// Starts unit (item, trial): its view, and (dma) the LDS DMA of its bottom
+// level into `buf` and, for a tile unit, of its blob into `aux`.  Nothing is
+// waited for: the caller waits (vmcnt) and barriers before reading LDS.
+// `ok` = the kernel instance can run the unit (the host validates every
+// schedule, validate_exec_plan; this guards the error flag): LDS buffer and
+// register rows, the metadata area, rows of exactly SMAX slots for SMAX <= 5
+// (unmasked full slots; kPack2: the p <= 32 rows).
+template <int SMAX, int RW>
+__device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t u, uint32_t* aux, float* buf, int tid,
+                                              bool dma, bool& ok)
+{
+    const int lane = tid & 63, wave = tid >> 6;
+    UnitCtx C;
+    C.U = unit_view(a, (int)(u / a.batch), (int)(u % a.batch));
+    const UnitView& U = C.U;
+    C.tile = U.mode == kModeTile;
+    C.table = U.blob != kNoBlob;
+    C.aux = aux;
     const int p = U.p;
-    const int nb = uni(M.nrows[U.levels]);
+    const int slots = merge_slots((uint32_t)p);
+    ok = U.levels <= kMaxLevels && p > 0 &&
+         ((SMAX <= 5 || SMAX == kPack2) ? slots == SMAX : (slots <= SMAX && slots != kPack2));
+    const int cap = min(lds_row_capacity((uint32_t)p, SMAX), kConeWaves * RW * row_pack(SMAX));
     const float* src;
     if (U.src == kSelLeaves) src = a.leaves + (uint64_t)U.trial * a.leaves_stride + U.src_off;
     else src = (U.src == kSelPing ? a.ping : a.pong) + (uint64_t)U.trial * a.buf_stride + U.buf_off;
     // transform blocks start 16-byte aligned and are padded to 4 floats
     const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(src, (((uint32_t)U.m * (uint32_t)p + 3u) & ~3u) * 4u);
-    if (U.mode != kModeTile) {
-        const uint32_t g0 = (uint32_t)U.node_start * (uint32_t)p;
-        const int al = (int)(g0 & 3u);
-        const int n = nb * p;
-        const int nchunks = (n + al + 3) >> 2;
-        F.len = n;
-        F.al = al;
-#pragma unroll
-        for (int k = 0; k < kFillChunks; ++k) {
-            const int c = tid + k * kConeBlock;
-            F.lo[k] = 0;
-            F.e[k] = c < nchunks ? 4 * c - al : n;
-            // chunks past the level load from an out-of-range offset (the
-            // buffer returns zeros; never landed): no exec-mask branch
-            const uint32_t off = c < nchunks ? (g0 - (uint32_t)al + 4u * (uint32_t)c) * 4u : 0x80000000u;
-            const auto q = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
-            F.v[k] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]),
-                                 __uint_as_float(q[3]));
-        }
+    if (!C.table) {
+        C.al = (int)(((uint32_t)U.node_start * (uint32_t)p) & 3u);
+        C.nruns = C.entries = C.nb = 0;
+        const int nch = (U.node_size * p + C.al + 3) >> 2;
+        ok = ok && !C.tile && U.node_size <= cap && 4 * nch <= kLdsBufFloats;
+        if (ok && dma)
+            dma_run(rs, ((uint32_t)U.node_start * (uint32_t)p - (uint32_t)C.al) * 4u, nch, buf, wave, kConeWaves, lane);
     } else {
-        const int amax = (p & 3) == 0 ? 0 : ((p & 1) == 0 ? 2 : 3);
-        const int nch = (p + amax + 3) >> 2;                 // chunks per row (upper bound)
-        const int totalc = nb * nch;
-        F.len = p;
-        F.al = 0;
-        int r = tid / nch;
-        int c = tid - r * nch;
-        const int dr = kConeBlock / nch, dc = kConeBlock - dr * nch;
-#pragma unroll
-        for (int k = 0; k < kFillChunks; ++k) {
-            const bool on = k * kConeBlock + tid < totalc;
-            const int rr = min(r, nb - 1);
-            const uint32_t g = (uint32_t)src_row[rr] * (uint32_t)p;
-            const int al = (int)(g & 3u);
-            const int e = 4 * c - al;
-            F.lo[k] = rr * p;
-            F.e[k] = on ? e : p;
-            const uint32_t off = (on && e < p) ? (g - (uint32_t)al + 4u * (uint32_t)c) * 4u : 0x80000000u;
-            const auto q = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
-            F.v[k] = make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]),
-                                 __uint_as_float(q[3]));
-            r += dr;
-            c += dc;
-            if (c >= nch) {
-                c -= nch;
-                ++r;
+        C.al = 0;
+        const const_u32_ptr blob = (const_u32_ptr)(uintptr_t)(a.blob + U.blob);
+        C.nruns = uni((int)blob[24]);
+        C.entries = uni((int)blob[25]);
+        C.nb = uni((int)blob[26]);
+        const int words = kBlobHeader + 4 * C.nruns + C.entries + C.nb;
+        ok = ok && C.nb <= cap && C.entries <= kDescEntries && words <= kAuxWords && C.nruns <= (1 << kMaxTileLevels);
+        if (ok && dma) {
+            // the blob: the last wave; the runs: all waves, round-robin
+            const __amdgpu_buffer_rsrc_t rb = buffer_rsrc(a.blob + U.blob, (uint32_t)((words + 3) & ~3) * 4u);
+            if (wave == kConeWaves - 1) dma_run(rb, 0u, (words + 3) >> 2, (float*)aux, 0, 1, lane);
+            for (int ri = wave; ri < C.nruns; ri += kConeWaves) {
+                const uint32_t g = blob[kBlobHeader + 4 * ri];
+                const int cb = (int)blob[kBlobHeader + 4 * ri + 1];
+                const int nch = (int)blob[kBlobHeader + 4 * ri + 2];
+                if (4 * (cb + nch) <= kLdsBufFloats) dma_run(rs, g * 4u, nch, buf + 4 * cb, 0, 1, lane);
             }
         }
     }
+    return C;
 }
 
-// Lands the staged chunks at base = data + F.al.  A chunk whose LDS address is
-// 16-byte aligned and lies wholly inside its segment is one ds_write_b128
-// (8x8-lane groups over 32 banks: conflict-free); the others (segment ends,
-// tile rows of odd phase) are written element-wise.
-__device__ __forceinline__ void fill_land(const Fill& F, float* base)
-{
-    const unsigned len = (unsigned)F.len;
-    const int al = F.al;
-#pragma unroll
-    for (int k = 0; k < kFillChunks; ++k) {
-        const int e = F.e[k];
-        float* row = base + F.lo[k];
-        const bool vec = e >= 0 && e + 3 < (int)len && ((F.lo[k] + e + al) & 3) == 0;
-        if (vec) {
-            *reinterpret_cast<float4*>(row + e) = F.v[k];
-        } else {
-            if ((unsigned)e < len) row[e] = F.v[k].x;
-            if ((unsigned)(e + 1) < len) row[e + 1] = F.v[k].y;
-            if ((unsigned)(e + 2) < len) row[e + 2] = F.v[k].z;
-            if ((unsigned)(e + 3) < len) row[e + 3] = F.v[k].w;
-        }
-    }
-}
-
-// Row descriptor (head row, tail row, roll shift) of output row r at level
-// l, as row indices of the level below; t = -1 for a carried leaf (size-1
-// node).
 // x mod p for 0 <= x < 2^22 and p >= 1 (roll shifts: x = s - t(s) < node
 // size): a float-reciprocal quotient, off by at most one, then corrected --
 // ~8 VALU instead of the ~35 of an integer remainder by a run-time p.
@@ -475,80 +362,53 @@ __device__ __forceinline__ int mod_small(int x, int p)
     return r >= p ? r - p : r;
 }
 
-__device__ __forceinline__ void row_desc(const UnitMeta& M, bool tile, int node_size, int l, int r, int p, int& h,
-                                         int& t, int& sh)
+// Row descriptor (head row, tail row, roll shift) of output row r at level
+// l of a whole unit (the node partition of its split tree), as row indices
+// of the level below; t = -1 for a carried leaf (size-1 node).
+__device__ __forceinline__ void row_desc(int node_size, int l, int r, int p, int& h, int& t, int& sh)
 {
-    if (tile) {
-        // the last of the level's 2^l ranges starting at or before r: l
-        // halving steps (uniform trip count)
-        const Range* lv = &M.ranges[(1 << l) - 1];
-        int lo = 0;
-        for (int step = (1 << l) >> 1; step > 0; step >>= 1)
-            if (lv[lo + step].base <= r) lo += step;
-        const Range R = lv[lo];
-        const int u = R.lo + (r - R.base);
-        const Range H = M.ranges[(2 << l) - 1 + 2 * lo];
-        const Range T = M.ranges[(2 << l) + 2 * lo];
-        const uint32_t hs = (uint32_t)R.size >> 1, ts = (uint32_t)R.size - hs;
-        const int hh = (int)merge_index(merge_coef(hs, (uint32_t)R.size), (uint32_t)u);
-        const int tt = (int)merge_index(merge_coef(ts, (uint32_t)R.size), (uint32_t)u);
-        h = H.base + hh - H.lo;
-        t = T.base + tt - T.lo;
-        sh = mod_small(u - tt, p);
-    } else {
-        int a0 = 0, sz = node_size;
-        for (int d = 0; d < l; ++d) {
-            if (sz > 1) {
-                const int hs = sz >> 1;
-                if (r - a0 < hs) sz = hs;
-                else {
-                    a0 += hs;
-                    sz -= hs;
-                }
+    int a0 = 0, sz = node_size;
+    for (int d = 0; d < l; ++d) {
+        if (sz > 1) {
+            const int hs = sz >> 1;
+            if (r - a0 < hs) sz = hs;
+            else {
+                a0 += hs;
+                sz -= hs;
             }
         }
-        if (sz <= 1) {
-            h = r;
-            t = -1;
-            sh = 0;
-        } else {
-            const int s = r - a0;
-            const uint32_t hs = (uint32_t)sz >> 1, ts = (uint32_t)sz - hs;
-            const int hh = (int)merge_index(merge_coef(hs, (uint32_t)sz), (uint32_t)s);
-            const int tt = (int)merge_index(merge_coef(ts, (uint32_t)sz), (uint32_t)s);
-            h = a0 + hh;
-            t = a0 + (int)hs + tt;
-            sh = mod_small(s - tt, p);
-        }
+    }
+    if (sz <= 1) {
+        h = r;
+        t = -1;
+        sh = 0;
+    } else {
+        const int s = r - a0;
+        const uint32_t hs = (uint32_t)sz >> 1, ts = (uint32_t)sz - hs;
+        const int hh = (int)merge_index(merge_coef(hs, (uint32_t)sz), (uint32_t)s);
+        const int tt = (int)merge_index(merge_coef(ts, (uint32_t)sz), (uint32_t)s);
+        h = a0 + hh;
+        t = a0 + (int)hs + tt;
+        sh = mod_small(s - tt, p);
     }
 }
 
 // Packed row descriptor: head row | tail row << 10 | shift << 20 (tail row
 // kCarried: a size-1 node carried unchanged).  Rows < 1023, shift < 4096.
-constexpr uint32_t kCarried = 1023;
+constexpr uint32_t kCarried = kCarriedRow;
 
 __device__ __forceinline__ uint32_t pack_desc(int h, int t, int sh)
 {
     return (uint32_t)h | ((t < 0 ? kCarried : (uint32_t)t) << 10) | ((uint32_t)sh << 20);
 }
 
-// First table entry of level l: levels 0..l-1 precede it.
-__device__ __forceinline__ int desc_offset(const UnitMeta& M, int l) { return uni(M.doff[l]); }
-
-// Descriptors of every output row of levels 0..L-1 (thread per entry).
-__device__ __forceinline__ void build_desc_table(const UnitMeta& M, uint32_t* desc, int entries, int p, int L,
-                                                 bool tile, int node_size, int tid)
+// Descriptor of output row r of level l: the tile table, or the node partition.
+__device__ __forceinline__ uint32_t unit_desc(const UnitCtx& C, int l, int r, int p)
 {
-    for (int idx = tid; idx < entries; idx += kConeBlock) {
-        int l = 0, r = idx;
-        while (r >= uni(M.nrows[l])) {
-            r -= uni(M.nrows[l]);
-            ++l;
-        }
-        int h, t, sh;
-        row_desc(M, tile, node_size, l, r, p, h, t, sh);
-        desc[idx] = pack_desc(h, t, sh);
-    }
+    if (C.table) return desc_table(C)[desc_offset(C, l) + r];
+    int h, t, sh;
+    row_desc(C.U.node_size, l, r, p, h, t, sh);
+    return pack_desc(h, t, sh);
 }
 
 typedef const __attribute__((address_space(3))) float* lds_cptr;
@@ -571,9 +431,8 @@ __device__ __forceinline__ float lds_ld(lds_cptr p) { return *(const volatile __
 // reference's copy).  Branch-free over rows and slots: rows i >= nr and bins
 // past p read in-bounds garbage that is never written back.
 template <int SMAX, int RW, bool CARRIED>
-__device__ __forceinline__ void merge_level_dense(const UnitMeta& M, const float* src, const uint32_t* desc,
-                                                  bool use_table, int p, int l, bool tile, int node_size, int lane,
-                                                  int wave, int nr, float (&v)[RW][SMAX])
+__device__ __forceinline__ void merge_level_dense(const UnitCtx& C, const float* src, int p, int l, int lane,
+                                                  int wave, int nr, float (&v)[RW][SMAX], const int* loff)
 {
     const int S = (p + 63) >> 6;
     // lane i unpacks the descriptor of the wave's i-th row into LDS float
@@ -581,19 +440,12 @@ __device__ __forceinline__ void merge_level_dense(const UnitMeta& M, const float
     // them with v_readlane, so no per-row scalar unpacking or multiplies
     int ho = 0, to = 0, sh = 0, car = 0;
     if (lane < nr) {
-        const int r = wave + kConeWaves * lane;
-        uint32_t d;
-        if (use_table) {
-            d = desc[desc_offset(M, l) + r];
-        } else {
-            int h, t, s;
-            row_desc(M, tile, node_size, l, r, p, h, t, s);
-            d = pack_desc(h, t, s);
-        }
+        const uint32_t d = unit_desc(C, l, wave + kConeWaves * lane, p);
         const uint32_t tc = (d >> 10) & 1023u;
         sh = (int)(d >> 20);
-        ho = (int)(d & 1023u) * p;
-        to = (tc == kCarried ? 0 : (int)tc * p) + sh;
+        // source rows: dense (stride p), or the bottom level's fill layout
+        ho = loff ? loff[d & 1023u] : (int)(d & 1023u) * p;
+        to = (tc == kCarried ? ho : (loff ? loff[tc] : (int)tc * p)) + sh;
         car = tc == kCarried;
     }
     const lds_cptr l1 = (lds_cptr)src + lane;
@@ -637,36 +489,24 @@ __device__ __forceinline__ void merge_level_dense(const UnitMeta& M, const float
 // Only levels whose nodes all have >= 2 rows (no carried size-1 nodes at
 // level l + 1) are fused.
 template <int SMAX, int RW>
-__device__ __forceinline__ void merge_level2_dense(const UnitMeta& M, const float* src, const uint32_t* desc,
-                                                   bool use_table, int p, int l, bool tile, int node_size, int lane,
-                                                   int wave, int nr, float (&v)[RW][SMAX])
+__device__ __forceinline__ void merge_level2_dense(const UnitCtx& C, const float* src, int p, int l, int lane,
+                                                   int wave, int nr, float (&v)[RW][SMAX], const int* loff)
 {
     const int S = (p + 63) >> 6;
     int o0 = 0, o1 = 0, o2 = 0, o3 = 0, s1 = 0, s2 = 0, s3 = 0;
     if (lane < nr) {
-        const int r = wave + kConeWaves * lane;
-        uint32_t d0, dh, dt;
-        if (use_table) {
-            d0 = desc[desc_offset(M, l) + r];
-            const int b1 = desc_offset(M, l + 1);
-            dh = desc[b1 + (int)(d0 & 1023u)];
-            dt = desc[b1 + (int)((d0 >> 10) & 1023u)];
-        } else {
-            int h, t, sh;
-            row_desc(M, tile, node_size, l, r, p, h, t, sh);
-            d0 = pack_desc(h, t, sh);
-            row_desc(M, tile, node_size, l + 1, h, p, h, t, sh);
-            dh = pack_desc(h, t, sh);
-            row_desc(M, tile, node_size, l + 1, (int)((d0 >> 10) & 1023u), p, h, t, sh);
-            dt = pack_desc(h, t, sh);
-        }
+        const uint32_t d0 = unit_desc(C, l, wave + kConeWaves * lane, p);
+        const uint32_t dh = unit_desc(C, l + 1, (int)(d0 & 1023u), p);
+        const uint32_t dt = unit_desc(C, l + 1, (int)((d0 >> 10) & 1023u), p);
         const int sh = (int)(d0 >> 20), sH = (int)(dh >> 20), sT = (int)(dt >> 20);
         int sTT = sh + sT;
         sTT = sTT >= p ? sTT - p : sTT;
-        o0 = (int)(dh & 1023u) * p;
-        o1 = (int)((dh >> 10) & 1023u) * p + sH;
-        o2 = (int)(dt & 1023u) * p + sh;
-        o3 = (int)((dt >> 10) & 1023u) * p + sTT;
+        // source rows: dense (stride p), or the bottom level's fill layout
+        const uint32_t r0 = dh & 1023u, r1 = (dh >> 10) & 1023u, r2 = dt & 1023u, r3 = (dt >> 10) & 1023u;
+        o0 = (loff ? loff[r0] : (int)r0 * p);
+        o1 = (loff ? loff[r1] : (int)r1 * p) + sH;
+        o2 = (loff ? loff[r2] : (int)r2 * p) + sh;
+        o3 = (loff ? loff[r3] : (int)r3 * p) + sTT;
         s1 = sH;
         s2 = sh;
         s3 = sTT;
@@ -703,25 +543,16 @@ __device__ __forceinline__ void merge_level2_dense(const UnitMeta& M, const floa
 // its own v_readlane and a select; otherwise as merge_level_dense (same
 // additions, same -0.0 carry masking).
 template <int RW, bool CARRIED>
-__device__ __forceinline__ void merge_level_packed(const UnitMeta& M, const float* src, const uint32_t* desc,
-                                                   bool use_table, int p, int l, bool tile, int node_size, int lane,
-                                                   int wave, int nr, float (&v)[RW][1])
+__device__ __forceinline__ void merge_level_packed(const UnitCtx& C, const float* src, int p, int l, int lane,
+                                                   int wave, int nr, float (&v)[RW][1], const int* loff)
 {
     int ho = 0, to = 0, sh = 0, car = 0;
     if (lane < nr) {
-        const int r = wave + kConeWaves * lane;
-        uint32_t d;
-        if (use_table) {
-            d = desc[desc_offset(M, l) + r];
-        } else {
-            int h, t, s;
-            row_desc(M, tile, node_size, l, r, p, h, t, s);
-            d = pack_desc(h, t, s);
-        }
+        const uint32_t d = unit_desc(C, l, wave + kConeWaves * lane, p);
         const uint32_t tc = (d >> 10) & 1023u;
         sh = (int)(d >> 20);
-        ho = (int)(d & 1023u) * p;
-        to = (tc == kCarried ? 0 : (int)tc * p) + sh;
+        ho = loff ? loff[d & 1023u] : (int)(d & 1023u) * p;
+        to = (tc == kCarried ? ho : (loff ? loff[tc] : (int)tc * p)) + sh;
         car = tc == kCarried;
     }
     const bool hi = lane >= 32;
@@ -845,11 +676,18 @@ __device__ __forceinline__ void write_rows_packed(float* base, float* dummy, con
 // written back.  With `st` set (a non-final pass), the output level goes from
 // the staging registers straight to global memory instead of back into LDS.
 template <int SMAX, int RW>
-__device__ __forceinline__ void merge_levels(const UnitMeta& M, float* base, const uint32_t* desc, bool use_table,
-                                             int p, int L, bool tile, int node_size, int tid, bool st,
+__device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int p, int L, int tid, bool st,
                                              __amdgpu_buffer_rsrc_t rs, uint32_t st_o0, uint32_t flags, float* dummy)
 {
     const int lane = tid & 63, wave = tid >> 6;
+    const bool tile = C.tile;
+    const int node_size = C.U.node_size;
+    // the first step reads the bottom level in its fill layout: through the
+    // blob's bottom-row offsets, or (whole unit without a blob) as dense rows
+    // at the block's 16-byte phase; every later level is dense rows (stride
+    // p) at base
+    const int* const loff = C.table ? bottom_offsets(C) : nullptr;
+    float* const src0 = C.table ? base : base + C.al;
     // deepest first; two levels per step (merge_level2_dense) once no level
     // below the step's output holds size-1 nodes, single steps before that
     // and for a last odd level
@@ -858,23 +696,26 @@ __device__ __forceinline__ void merge_levels(const UnitMeta& M, float* base, con
         // size-1 nodes exist at depth l only in whole units with node_size >> l < 2
         const bool two = fuse && l >= 1 && (tile || (node_size >> l) >= 2);
         const int lo = two ? l - 1 : l;          // output level of this step
-        const int orows = uni(M.nrows[lo]);
+        const int orows = rows_at(C, lo);
         const int nr = uni(orows > wave ? (orows - wave + kConeWaves - 1) / kConeWaves : 0);
         constexpr int S = slot_count(SMAX);
         float v[RW][S];
         const bool carried = !tile && (node_size >> l) < 2;
+        const bool first = l == L - 1;
+        const float* src = first ? src0 : base;
+        const int* lo_src = first ? loff : nullptr;
         if constexpr (SMAX == kPack2) {
             if (carried)
-                merge_level_packed<RW, true>(M, base, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
+                merge_level_packed<RW, true>(C, src, p, l, lane, wave, nr, v, lo_src);
             else
-                merge_level_packed<RW, false>(M, base, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
+                merge_level_packed<RW, false>(C, src, p, l, lane, wave, nr, v, lo_src);
         } else {
             if (two)
-                merge_level2_dense<S, RW>(M, base, desc, use_table, p, lo, tile, node_size, lane, wave, nr, v);
+                merge_level2_dense<S, RW>(C, src, p, lo, lane, wave, nr, v, lo_src);
             else if (carried)
-                merge_level_dense<S, RW, true>(M, base, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
+                merge_level_dense<S, RW, true>(C, src, p, l, lane, wave, nr, v, lo_src);
             else
-                merge_level_dense<S, RW, false>(M, base, desc, use_table, p, l, tile, node_size, lane, wave, nr, v);
+                merge_level_dense<S, RW, false>(C, src, p, l, lane, wave, nr, v, lo_src);
         }
         l = lo - 1;
         if (lo == 0 && st) {
@@ -904,7 +745,7 @@ __device__ __forceinline__ void merge_levels(const UnitMeta& M, float* base, con
 constexpr int kSnrWin = 12;
 // S/N chunk columns per lane held in registers (and the window path), by the
 // register budget of the block size
-constexpr int kSnrMaxChunk = kConeBlock >= 1024 || kConeWgsPerCu == 3 ? 9 : 17;
+constexpr int kSnrMaxChunk = 17;
 
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v)
@@ -1286,112 +1127,132 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
 #endif
 
 // One kernel per merge slot width SMAX (units with ceil(p/64) <= SMAX), so each
-// gets its own register allocation.  min 4 waves per SIMD: <= 128 VGPRs, two
-// workgroups per CU.
+// gets its own register allocation.  Persistent: a workgroup takes units u =
+// blockIdx.x, blockIdx.x + gridDim.x, ... (unit u = item u / batch, trial u %
+// batch; items are sorted longest first).  One level buffer (kConeBuffers =
+// 1, two workgroups per CU): a unit's DMA is waited for at its start, the
+// CU's other workgroup filling the wait; two buffers (one workgroup per CU):
+// while unit u is merged in one, unit u + gridDim.x streams into the other.
+//   begin(u) [DMA] | wait | merge(u) | store or S/N(u)
 template <int SMAX, int RWT = 0>
 __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(ConeArgs a)
 {
     constexpr int RW = RWT ? RWT : merge_rows_per_wave(SMAX);   // register rows per wave
-#ifdef RT_STAMPS
-    unsigned long long tl[kStampMarks] = {};
-    tl[0] = __builtin_amdgcn_s_memtime();
-#endif
-    __shared__ __attribute__((aligned(16))) float data[kLdsDataFloats + kLdsPadFloats];
-    __shared__ UnitMeta M;
-    __shared__ uint32_t desc[kDescEntries];
-    __shared__ int src_row[kMaxRows];
+    __shared__ __attribute__((aligned(16))) float data[kConeBuffers][kLdsBufFloats + kLdsPadFloats];
+    __shared__ __attribute__((aligned(16))) uint32_t aux[kConeBuffers][kAuxWords];   // tile units: the host blob
     __shared__ int wl[kMaxWidths];   // boxcar widths: LDS reads never wait on the S/N stores in flight
     __shared__ float whb[2 * kMaxWidths];   // S/N: h + b and b per width
 
     const int tid = threadIdx.x;
-    // grid (items, trials): no division to split a flat unit index
-    const int item = (int)blockIdx.x, trial = (int)blockIdx.y;
-    if (item >= (int)a.num_items || trial >= (int)a.batch) return;
-    const int u = trial * (int)a.num_items + item;   // unit record index (diagnostic stamps)
-    (void)u;
-    if (tid < (int)a.num_widths) wl[tid] = (int)a.widths[tid];   // visible after setup's barriers
-    setup_unit(a, item, trial, M, src_row, tid);
-    RT_MARK(1);
-    const UnitView U = read_view(M);
-    const int p = U.p;
-    const int L = U.levels;
-    const bool tile = U.mode == kModeTile;
-    bool ok = uni(M.nrows[L]) * p <= kLdsDataFloats;
-    // SMAX <= 5 variants assume rows of exactly SMAX slots (unmasked full slots)
-    // (kPack2 runs exactly the p <= 32 rows)
-    ok = ok && ((SMAX <= 5 || SMAX == kPack2) ? merge_slots((uint32_t)p) == SMAX
-                                              : (merge_slots((uint32_t)p) <= SMAX && merge_slots((uint32_t)p) != kPack2));
-    for (int l = 0; l <= L; ++l)
-        ok = ok && uni(M.nrows[l]) <= lds_row_capacity((uint32_t)p, SMAX) &&
-             uni(M.nrows[l]) <= kConeWaves * RW * row_pack(SMAX);
-    if (!ok) {
-        if (tid == 0 && a.error_flag) atomicOr(a.error_flag, 1);
-        return;
-    }
-    Fill F;
-    fill_issue(a, M, U, src_row, tid, F);
-    RT_MARK(2);
-    // row descriptors of every level while the loads are in flight
-    const int entries = desc_offset(M, L);
-    const bool use_table = entries <= kDescEntries;
-    if (use_table && !(a.flags & kConeDiagNoDesc)) build_desc_table(M, desc, entries, p, L, tile, U.node_size, tid);
-    RT_MARK(3);
-    float* const base = data + uni(F.al);   // the filled level: dense rows, stride p
-    if (!(a.flags & kConeDiagNoLand)) fill_land(F, base);
-    else if (F.v[0].x == 12345.678f) base[tid] = F.v[0].y;   // keep the loads alive
-    lds_barrier();
-    RT_MARK(4);
-    // ---- merge levels, deepest first; a non-final pass stores its output
-    // level straight from registers (st), a final pass keeps it in LDS for
-    // the S/N epilogue
-    const bool st = U.dst != kSelSnr;
-    const bool st_regs = st && (a.flags & kConeStoreFromRegs);
-    const float* dst = (U.dst == kSelPing ? a.ping : a.pong) + (uint64_t)U.trial * a.buf_stride + U.buf_off;
-    const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(dst, (((uint32_t)U.m * (uint32_t)p + 3u) & ~3u) * 4u);
-    const uint32_t o0 = (uint32_t)(U.node_start + U.s0) * (uint32_t)p * 4u;
-    if (L > 0 && !(a.flags & kConeDiagNoMerge))
-        merge_levels<SMAX, RW>(M, base, desc, use_table, p, L, tile, U.node_size, tid, st_regs,
-                                                      rs, o0, a.flags, data + kLdsDataFloats + 4 + (tid & 63));
-    RT_MARK(5);
-    const int n0 = uni(M.nrows[0]);
-    // the output level, in place in the dense rows at base
-    float* const obuf = base;
-    const int ostride = p;
-    if (st) {
-        if (L == 0 || !st_regs) {
-            // ---- store the output level from LDS (a single leaf row, or A/B)
-            for (int r = 0; r < n0; ++r)
-                for (int j = tid; j < p; j += kConeBlock)
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(obuf[r * ostride + j]), rs,
-                                                          (int)(o0 + (uint32_t)(r * p + j) * 4u), 0, 0);
-        }
-    } else {
+    const uint32_t total = a.num_items * a.batch;
+    uint32_t u = blockIdx.x;
+    if (u >= total) return;
+    if (tid < (int)a.num_widths) wl[tid] = (int)a.widths[tid];   // visible after the first barrier
+    const bool dma = !(a.flags & kConeDiagNoLand);
+    int b = 0;
+    bool ok;
+    UnitCtx C = unit_begin<SMAX, RW>(a, u, aux[0], data[0], tid, dma, ok);
+    for (;;) {
 #ifdef RT_STAMPS
-        if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX>(a, U, obuf, ostride, wl, n0, tid, whb, tl);
+        unsigned long long tl[kStampMarks] = {};
+        tl[0] = __builtin_amdgcn_s_memtime();
+#endif
+        const UnitView& U = C.U;
+        const int p = U.p;
+        const int L = U.levels;
+        float* const buf = data[b];
+        // every wave waits for its own DMA (the previous unit's stores count
+        // in the same in-order counter), the barrier publishes all of them
+        __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)
+        lds_barrier();
+        RT_MARK(1);
+        const uint32_t un = u + gridDim.x;
+        const bool has_next = un < total;
+        bool ok_next = false;
+        UnitCtx Cn;
+        if (kConeBuffers == 2 && has_next) Cn = unit_begin<SMAX, RW>(a, un, aux[b ^ 1], data[b ^ 1], tid, dma, ok_next);
+        RT_MARK(2);
+        if (!ok) {
+            if (tid == 0 && a.error_flag) atomicOr(a.error_flag, 1);
+        } else {
+            // merge levels, deepest first; a non-final pass stores its output
+            // level straight from registers (st), a final pass keeps it in LDS
+            // for the S/N epilogue
+            const bool st = U.dst != kSelSnr;
+            const bool st_regs = st && (a.flags & kConeStoreFromRegs);
+            const float* dst = (U.dst == kSelPing ? a.ping : a.pong) + (uint64_t)U.trial * a.buf_stride + U.buf_off;
+            const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(dst, (((uint32_t)U.m * (uint32_t)p + 3u) & ~3u) * 4u);
+            const uint32_t o0 = (uint32_t)(U.node_start + U.s0) * (uint32_t)p * 4u;
+            if (L > 0 && !(a.flags & kConeDiagNoMerge))
+                merge_levels<SMAX, RW>(C, buf, p, L, tid, st_regs, rs, o0, a.flags, buf + kLdsBufFloats + 4 + (tid & 63));
+            RT_MARK(3);
+            const int n0 = rows_at(C, 0);
+            // the output level: dense rows from the buffer start, or (no merge
+            // level) the single bottom row where the DMA left it
+            float* const obase = L > 0 ? buf : buf + (C.table ? uni(bottom_offsets(C)[0]) : C.al);
+            if (st) {
+                if (L == 0 || !st_regs) {
+                    for (int r = 0; r < n0; ++r)
+                        for (int j = tid; j < p; j += kConeBlock)
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(obase[r * p + j]), rs,
+                                                                  (int)(o0 + (uint32_t)(r * p + j) * 4u), 0, 0);
+                }
+            } else {
+#ifdef RT_STAMPS
+                if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX>(a, U, obase, p, wl, n0, tid, whb, tl);
 #else
-        if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX>(a, U, obuf, ostride, wl, n0, tid, whb, nullptr);
+                if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX>(a, U, obase, p, wl, n0, tid, whb, nullptr);
 #endif
-    }
+            }
+        }
+        lds_barrier();                        // the level buffer is free
 #ifdef RT_STAMPS
-    if (tid == 0 && a.stamps) {
-        RT_MARK(6);
-        unsigned long long* e = a.stamps + (uint64_t)kStampRecWords * (uint64_t)u;
-        const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));     // HW_REG_HW_ID
-        const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11));   // HW_REG_XCC_ID
-        e[0] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+        if (tid == 0 && a.stamps) {
+            RT_MARK(4);
+            unsigned long long* e = a.stamps + (uint64_t)kStampRecWords * (uint64_t)u;
+            const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));     // HW_REG_HW_ID
+            const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11));   // HW_REG_XCC_ID
+            e[0] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
 #pragma unroll
-        for (int i = 0; i < kStampMarks; ++i) e[1 + i] = tl[i];
-        e[1 + kStampMarks] = (unsigned long long)p | ((unsigned long long)L << 16) |
-                             ((unsigned long long)U.mode << 24) | ((unsigned long long)n0 << 32) |
-                             ((unsigned long long)(U.dst == kSelSnr) << 48);
-    }
+            for (int i = 0; i < kStampMarks; ++i) e[1 + i] = tl[i];
+            e[1 + kStampMarks] = (unsigned long long)p | ((unsigned long long)L << 16) |
+                                 ((unsigned long long)U.mode << 24) | ((unsigned long long)rows_at(C, 0) << 32) |
+                                 ((unsigned long long)(U.dst == kSelSnr) << 48);
+        }
 #endif
+        if (!has_next) break;
+        u = un;
+        if (kConeBuffers == 2) {
+            b ^= 1;
+            C = Cn;
+            ok = ok_next;
+        } else {
+            C = unit_begin<SMAX, RW>(a, u, aux[0], data[0], tid, dma, ok);
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0): no DMA outstanding at exit
 }
 
+// Persistent grid: kConeWgsPerCu workgroups per CU (RIPTIDE_AMD_CONE_PERSIST=0:
+// one workgroup per unit, for A/B).
 hipError_t launch_cone(const ConeArgs& args, uint32_t smax, uint32_t rw, hipStream_t s)
 {
     if (!args.num_items || !args.batch) return hipSuccess;
-    const dim3 g(args.num_items, args.batch), b(kConeBlock);
+    const uint64_t total = (uint64_t)args.num_items * args.batch;
+    if (total > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    uint64_t grid = (uint64_t)cus * kConeWgsPerCu;
+    // persistent workgroups only with two level buffers (their point is the
+    // prefetch); with one buffer a workgroup per unit keeps both of a CU's
+    // workgroup slots busy to the end of the launch (measured: 10.37 vs 11.55
+    // ms per cfg2 trial).  RIPTIDE_AMD_CONE_PERSIST=0/1 overrides.
+    static const bool persist = [] {
+        const char* e = std::getenv("RIPTIDE_AMD_CONE_PERSIST");
+        return e ? std::atoi(e) != 0 : kConeBuffers == 2;
+    }();
+    if (!persist || grid > total) grid = total;
+    const dim3 g((uint32_t)grid), b(kConeBlock);
     switch (smax) {
     case 1:
         switch (rw) {

@@ -133,6 +133,9 @@ ConeNeed cone_need(uint32_t node_size, uint32_t s0, uint32_t s1, int levels, uin
     auto account = [&](const std::vector<R>& lv) {
         int rows = 0;
         for (const R& r : lv) rows += (int)(r.hi - r.lo + 1);
+        need.entries += need.rows_bottom; // descriptors of the level above the one accounted now
+        need.rows_bottom = rows;          // the last level accounted is the cone's bottom
+        need.runs_bottom = (int)lv.size();
         need.max_rows = std::max(need.max_rows, rows);
         need.max_floats = std::max(need.max_floats, rows * (int)p);
         need.ranges += (int)lv.size();
@@ -162,7 +165,8 @@ ConeNeed cone_need(uint32_t node_size, uint32_t s0, uint32_t s1, int levels, uin
 static bool fits(const ConeNeed& n, uint32_t p, int smax)
 {
     return !n.degenerate && n.max_rows <= lds_row_capacity(p, smax) && n.max_floats <= kLdsDataFloats &&
-           n.ranges <= kMaxRanges;
+           n.ranges <= kMaxRanges && 4 * fill_chunks_bound(n.rows_bottom, (int)p, n.runs_bottom) <= kLdsBufFloats &&
+           n.entries <= kDescEntries;
 }
 
 // Per-transform schedule: list of passes, each a list of (node, tile, levels).
@@ -391,7 +395,128 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
         g0 = g1;
         ++group;
     }
+    // host-built metadata of the tile items (trial-independent, shared by a
+    // launch's whole batch)
+    for (ConeItem& it : out.items) {
+        it.pad = kNoBlob;
+        // whole units: a descriptor table only when it fits the LDS area
+        // (otherwise the kernel derives the node partition on the fly)
+        if (it.mode != kModeTile &&
+            ((uint64_t)it.levels * it.node_size > (uint64_t)kDescEntries || it.node_size > (uint32_t)kMaxRows))
+            continue;
+        it.pad = (uint32_t)out.blob.size();
+        build_tile_blob(it, out.xf[it.xform].p, out.blob);
+    }
     validate_exec_plan(out, snr_epilogue);
+}
+
+void build_tile_blob(const ConeItem& it, uint32_t p, std::vector<uint32_t>& out)
+{
+    struct R { uint32_t size, lo, hi; uint32_t start; uint32_t base; };
+    const int L = it.levels;
+    const bool tile = it.mode == kModeTile;
+    // level l: the row ranges of the unit (tile: 2^l ranges of the dependency
+    // cone, children of range j at 2j (head) and 2j + 1 (tail) -- the planner
+    // guarantees every node above the bottom has >= 2 rows; whole unit: the
+    // node, one range per level)
+    std::vector<std::vector<R>> lv(L + 1);
+    lv[0].push_back({it.node_size, it.s0, it.s1 - 1, it.node_start, 0});
+    for (int l = 1; l <= L; ++l) {
+        if (!tile) {
+            lv[l].push_back(lv[0][0]);
+            continue;
+        }
+        for (const R& r : lv[l - 1]) {
+            const uint32_t sh = r.size >> 1, st = r.size - sh;
+            const float kh = merge_coef(sh, r.size), kt = merge_coef(st, r.size);
+            lv[l].push_back({sh, merge_index(kh, r.lo), merge_index(kh, r.hi), r.start, 0});
+            lv[l].push_back({st, merge_index(kt, r.lo), merge_index(kt, r.hi), r.start + sh, 0});
+        }
+    }
+    uint32_t nrows[kMaxLevels + 1] = {}, doff[kMaxLevels + 1] = {};
+    uint32_t entries = 0;
+    for (int l = 0; l <= L; ++l) {
+        uint32_t b = 0;
+        for (R& r : lv[l]) {
+            r.base = b;
+            b += r.hi - r.lo + 1;
+        }
+        nrows[l] = b;
+        doff[l] = entries;
+        if (l < L) entries += b;
+    }
+    const size_t o = out.size();
+    const uint32_t nruns = (uint32_t)lv[L].size(), nb = nrows[L];
+    const size_t words = kBlobHeader + 4 * (size_t)nruns + entries + nb;
+    out.resize(o + ((words + 3) & ~(size_t)3), 0u);
+    uint32_t* w = out.data() + o;
+    for (int l = 0; l <= L; ++l) {
+        w[l] = nrows[l];
+        w[12 + l] = doff[l];
+    }
+    w[24] = nruns;
+    w[25] = entries;
+    w[26] = nb;
+    uint32_t* run = w + kBlobHeader;
+    uint32_t* desc = run + 4 * nruns;
+    uint32_t* loff = desc + entries;
+    for (int l = 0; l < L; ++l) {
+        if (!tile) {
+            // whole unit (cone_kernel row_desc): row r of depth l lies in the
+            // depth-l node of the rows >> 1 split tree; size-1 nodes are carried
+            for (uint32_t r = 0; r < nrows[l]; ++r) {
+                uint32_t a0 = 0, sz = it.node_size;
+                for (int d = 0; d < l; ++d)
+                    if (sz > 1) {
+                        const uint32_t hs = sz >> 1;
+                        if (r - a0 < hs) sz = hs;
+                        else {
+                            a0 += hs;
+                            sz -= hs;
+                        }
+                    }
+                uint32_t word;
+                if (sz <= 1) {
+                    word = r | (kCarriedRow << 10);
+                } else {
+                    const uint32_t s = r - a0, hs = sz >> 1, ts = sz - hs;
+                    const uint32_t hh = merge_index(merge_coef(hs, sz), s);
+                    const uint32_t tt = merge_index(merge_coef(ts, sz), s);
+                    word = (a0 + hh) | ((a0 + hs + tt) << 10) | (((s - tt) % p) << 20);
+                }
+                desc[doff[l] + r] = word;
+            }
+            continue;
+        }
+        // tile unit: output row r of level l within range j of its level
+        size_t j = 0;
+        for (uint32_t r = 0; r < nrows[l]; ++r) {
+            while (j + 1 < lv[l].size() && lv[l][j + 1].base <= r) ++j;
+            const R& g = lv[l][j];
+            const uint32_t u = g.lo + (r - g.base);
+            const R& H = lv[l + 1][2 * j];
+            const R& T = lv[l + 1][2 * j + 1];
+            const uint32_t hs = g.size >> 1, ts = g.size - hs;
+            const uint32_t hh = merge_index(merge_coef(hs, g.size), u);
+            const uint32_t tt = merge_index(merge_coef(ts, g.size), u);
+            const uint32_t h = H.base + hh - H.lo, t = T.base + tt - T.lo;
+            const uint32_t sh = (u - tt) % p;
+            desc[doff[l] + r] = h | (t << 10) | (sh << 20);
+        }
+    }
+    // bottom level: one DMA run per range, each at its own 16-byte phase
+    uint32_t cb = 0;
+    for (uint32_t ri = 0; ri < nruns; ++ri) {
+        const R& g = lv[L][ri];
+        const uint32_t first = (g.start + g.lo) * p;
+        const uint32_t al = first & 3u, cnt = g.hi - g.lo + 1;
+        const uint32_t nch = (cnt * p + al + 3) >> 2;
+        run[4 * ri] = first - al;
+        run[4 * ri + 1] = cb;
+        run[4 * ri + 2] = nch;
+        for (uint32_t r = 0; r < cnt; ++r) loff[g.base + r] = 4 * cb + al + r * p;
+        cb += nch;
+    }
 }
 
 void validate_exec_plan(const ExecPlan& ex, bool snr_epilogue)
@@ -425,6 +550,13 @@ void validate_exec_plan(const ExecPlan& ex, bool snr_epilogue)
                     throw std::runtime_error("schedule: whole node exceeds the LDS budget");
                 rows = (int)it.node_size;
             }
+            const ConeNeed need = it.mode == kModeTile ? cone_need(it.node_size, it.s0, it.s1, it.levels, X.p)
+                                                       : ConeNeed{};
+            const int bottom = it.mode == kModeTile ? need.rows_bottom : (int)it.node_size;
+            if (4 * fill_chunks_bound(bottom, (int)X.p, it.mode == kModeTile ? 1 << it.levels : 1) > kLdsBufFloats)
+                throw std::runtime_error("schedule: unit fill exceeds the LDS level buffer");
+            if (it.mode == kModeTile && (need.entries > kDescEntries || it.pad == kNoBlob))
+                throw std::runtime_error("schedule: tile descriptor table exceeds its LDS area");
             // the launch's kernel instance stages enough register rows for every level
             const int rw = L.rw ? (int)L.rw : merge_rows_per_wave((int)L.smax);
             if (rows > kConeWaves * rw * row_pack((int)L.smax) || rows > lds_row_capacity(X.p, (int)L.smax))

@@ -60,11 +60,25 @@ struct Launch {
 
 struct ExecPlan {
     std::vector<FfaXform> xf;
-    std::vector<ConeItem> items;
+    std::vector<ConeItem> items;     // tile items: ConeItem::pad = word offset of their blob
     std::vector<Launch> launches;
+    std::vector<uint32_t> blob;      // host-built metadata of every tile item (build_tile_blob)
     uint64_t scratch_floats = 0;     // per ping/pong buffer, per trial
     uint32_t max_passes = 0;
 };
+
+// Tile-unit metadata built on the host once per plan (the cone kernel reads
+// it, never recomputes it): the dependency cone's range tree flattened into
+// rows per level, the row-descriptor table of every level (head row | tail
+// row << 10 | roll shift << 20, transforms.hpp:13-27 restated per row), the
+// LDS DMA runs of the bottom level and the LDS float offset of every bottom
+// row in that fill layout.  Blob layout (uint32 words, 16-byte aligned):
+//   [0, 12)  rows of levels 0..L        [12, 24) first descriptor of each level
+//   [24] runs  [25] descriptor entries  [26] bottom rows  [27, 32) 0
+//   [32, 32 + 4 runs)  per run: first float of the run in the transform block
+//                      (16-byte aligned), first chunk, chunks, 0
+//   then the descriptor table (entries words), then the bottom-row offsets.
+void build_tile_blob(const ConeItem& it, uint32_t p, std::vector<uint32_t>& out);
 
 // Schedule a list of transforms (p, m, rows_eval, src_off, snr_row, stdnoise
 // filled in by the caller).  With snr_epilogue the last pass of every
@@ -87,7 +101,7 @@ void validate_exec_plan(const ExecPlan& ex, bool snr_epilogue);
 constexpr uint64_t kMaxBlockBytes = 1ull << 31;
 
 // Dependency-cone footprint of one tile (host mirror of the device range tree).
-struct ConeNeed { int max_rows = 0; int max_floats = 0; int ranges = 0; bool degenerate = false; };
+struct ConeNeed { int max_rows = 0; int max_floats = 0; int ranges = 0; int rows_bottom = 0; int runs_bottom = 0; int entries = 0; bool degenerate = false; };
 ConeNeed cone_need(uint32_t node_size, uint32_t s0, uint32_t s1, int levels, uint32_t p);
 
 }  // namespace rt

@@ -21,7 +21,7 @@ sys.path.insert(0, REPO)
 
 MARKS = 11
 REC = MARKS + 2
-PHASES = ["setup", "issue", "desc", "wait", "merge", "tail"]
+PHASES = ["wait", "begin_next", "merge", "tail"]
 
 
 def main():
@@ -54,13 +54,13 @@ def analyse(e):
     xcc = (e[:, 0] >> 32) & 0xF
     cu = ((hw >> 8) & 0xF) | (((hw >> 12) & 1) << 4) | (((hw >> 13) & 0x7) << 5) | (xcc << 8)
     t = e[:, 1:1 + MARKS]
-    tend = t[:, 6]
+    tend = t[:, len(PHASES)]
     shape = e[:, 1 + MARKS]
     snr = (shape >> 48) & 1
     mode = (shape >> 24) & 0xFF
     lv = (shape >> 16) & 0xFF
     n0 = (shape >> 32) & 0xFFFF
-    ph = np.diff(t[:, :7], axis=1)
+    ph = np.diff(t[:, :len(PHASES) + 1], axis=1)
     out = {"units": int(e.shape[0]), "distinct_cus": int(np.unique(cu).size),
            "mean_cycles": dict(zip(PHASES, ph.mean(axis=0).round(0).tolist())),
            "mean_total": float((tend - t[:, 0]).mean())}
@@ -77,9 +77,9 @@ def analyse(e):
     m = (snr == 1) & np.all(t[:, 7:11] > 0, axis=1)
     if m.any():
         sn = t[m]
-        out["snr_pass0"] = {"prefix": float((sn[:, 7] - sn[:, 5]).mean()), "barrier": float((sn[:, 8] - sn[:, 7]).mean()),
+        out["snr_pass0"] = {"prefix": float((sn[:, 7] - sn[:, 3]).mean()), "barrier": float((sn[:, 8] - sn[:, 7]).mean()),
                             "window": float((sn[:, 9] - sn[:, 8]).mean()), "widths": float((sn[:, 10] - sn[:, 9]).mean()),
-                            "rest": float((sn[:, 6] - sn[:, 10]).mean())}
+                            "rest": float((tend[m] - sn[:, 10]).mean())}
     # per-CU residency and idle gaps (s_memtime is per XCD: compare within a CU only)
     occ = np.zeros(4)
     gaps = []
