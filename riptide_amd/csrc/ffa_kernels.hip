@@ -745,6 +745,9 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
 constexpr int kSnrWin = 12;
 // S/N chunk columns per lane held in registers (and the window path), by the
 // register budget of the block size
+// (33, G = 8 lanes per row for p <= 264 -- one 64-row pass per final-pass
+// unit -- measured 10.08 vs 10.15 ms per cfg2 trial but its column masks
+// spill ~300 SGPRs, which slows the merge: kept at 17)
 constexpr int kSnrMaxChunk = 17;
 
 template <int CTRL>
@@ -1034,7 +1037,8 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
         whb[2 * tid + 1] = b;
     }
     // G lanes per row: the smallest power of two >= 8 whose chunks fit
-    // kSnrMaxChunk columns (17 at G = 64); chunk lengths odd
+    // kSnrMaxChunk columns; chunk lengths odd (the G chunks of a row start
+    // on distinct banks)
     int G = 8;
     while (G < 64 && (((p + G - 1) / G) | 1) > kSnrMaxChunk) G <<= 1;
     int c = (p + G - 1) / G;
@@ -1166,8 +1170,10 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
         __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)
         lds_barrier();
         RT_MARK(1);
+        // one buffer: one unit per workgroup (a compile-time single pass, so
+        // nothing is hoisted out of a unit loop into long-lived registers)
         const uint32_t un = u + gridDim.x;
-        const bool has_next = un < total;
+        const bool has_next = kConeBuffers == 2 && un < total;
         bool ok_next = false;
         UnitCtx Cn;
         if (kConeBuffers == 2 && has_next) Cn = unit_begin<SMAX, RW>(a, un, aux[b ^ 1], data[b ^ 1], tid, dma, ok_next);
@@ -1244,12 +1250,12 @@ hipError_t launch_cone(const ConeArgs& args, uint32_t smax, uint32_t rw, hipStre
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     uint64_t grid = (uint64_t)cus * kConeWgsPerCu;
     // persistent workgroups only with two level buffers (their point is the
-    // prefetch); with one buffer a workgroup per unit keeps both of a CU's
-    // workgroup slots busy to the end of the launch (measured: 10.37 vs 11.55
-    // ms per cfg2 trial).  RIPTIDE_AMD_CONE_PERSIST=0/1 overrides.
+    // prefetch; RIPTIDE_AMD_CONE_PERSIST=0 turns them off); with one buffer a
+    // workgroup per unit keeps both of a CU's workgroup slots busy to the end
+    // of the launch (measured: 10.37 vs 11.55 ms per cfg2 trial persistent).
     static const bool persist = [] {
         const char* e = std::getenv("RIPTIDE_AMD_CONE_PERSIST");
-        return e ? std::atoi(e) != 0 : kConeBuffers == 2;
+        return kConeBuffers == 2 && (e ? std::atoi(e) != 0 : true);
     }();
     if (!persist || grid > total) grid = total;
     const dim3 g((uint32_t)grid), b(kConeBlock);
