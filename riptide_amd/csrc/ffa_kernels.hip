@@ -745,10 +745,10 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
 constexpr int kSnrWin = 12;
 // S/N chunk columns per lane held in registers (and the window path), by the
 // register budget of the block size
-// (33, G = 8 lanes per row for p <= 264 -- one 64-row pass per final-pass
-// unit -- measured 10.08 vs 10.15 ms per cfg2 trial but its column masks
-// spill ~300 SGPRs, which slows the merge: kept at 17)
-constexpr int kSnrMaxChunk = 17;
+#ifndef RT_SNR_MAX_CHUNK
+#define RT_SNR_MAX_CHUNK 17
+#endif
+constexpr int kSnrMaxChunk = RT_SNR_MAX_CHUNK;
 
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v)
@@ -1042,7 +1042,7 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
     int G = 8;
     while (G < 64 && (((p + G - 1) / G) | 1) > kSnrMaxChunk) G <<= 1;
     int c = (p + G - 1) / G;
-    if (c < kSnrChunk) c |= 1;
+    if (c < kSnrMaxChunk) c |= 1;
     const uint32_t nw = a.num_widths;
     float* snr = a.snr + (uint64_t)U.trial * a.snr_stride + (U.snr_row + (uint64_t)U.s0) * (uint64_t)nw;
     if (c <= kSnrMaxChunk) {
