@@ -187,6 +187,14 @@ struct DevicePlan {
             d.src = it.src;
             d.dst = it.dst;
             d.pad = it.pad;
+            if (it.pad != kNoBlob) {
+                const uint32_t* h = ex.blob.data() + it.pad;
+                d.nruns = h[kHdrRuns];
+                d.entries = h[kHdrEntries];
+                d.nb = h[kHdrBottom];
+                d.slot_words = h[kHdrSlotWords];
+                d.run_off = h[kHdrRunOff];
+            }
             u[i] = d;
         }
         // Test hook (RIPTIDE_AMD_DEBUG_CORRUPT_UNIT=1): give the first whole-node

@@ -41,15 +41,22 @@ namespace rt {
 #endif
 constexpr int kConeBuffers = RT_CONE_BUFFERS;
 static_assert(kConeBuffers == 1 || kConeBuffers == 2, "RT_CONE_BUFFERS is 1 or 2");
-constexpr int kConeWgsPerCu = kConeBuffers == 2 ? 1 : 2;
-constexpr int kConeBlock = kConeBuffers == 2 ? 1024 : 512;
+// one buffer: workgroups per CU (2: 512 threads and a 71 KiB buffer each;
+// 4: 256 threads and a 35 KiB buffer each -- smaller units, more of them in
+// flight per CU)
+#ifndef RT_CONE_WGS
+#define RT_CONE_WGS 2
+#endif
+static_assert(RT_CONE_WGS == 2 || RT_CONE_WGS == 4, "RT_CONE_WGS is 2 or 4");
+constexpr int kConeWgsPerCu = kConeBuffers == 2 ? 1 : RT_CONE_WGS;
+constexpr int kConeBlock = kConeBuffers == 2 ? 1024 : (kConeWgsPerCu == 2 ? 512 : 256);
 constexpr int kConeWaves = kConeBlock / 64;
 constexpr int kConeWavesPerSimd = kConeWgsPerCu * kConeWaves / 4;
-constexpr int kLdsBufFloats = kConeBuffers == 2 ? 17920 : 18176;   // one level buffer: a unit's fill (16-byte chunks, runs per range)
+constexpr int kLdsBufFloats = kConeBuffers == 2 ? 17920 : (kConeWgsPerCu == 2 ? 18176 : 8704);   // one level buffer: a unit's fill (16-byte chunks, runs per range)
 constexpr int kLdsDataFloats = kLdsBufFloats - 256;   // rows x p of any level (the rest: per-range 16-byte phase slack)
 constexpr int kLdsPadFloats = 128;          // slack read (never used) by the unused slots of the last row
-constexpr int kMaxRows = 384;               // rows per level (row-offset table, descriptors)
-constexpr int kDescEntries = 1024;          // row-descriptor table (all levels of a unit)
+constexpr int kMaxRows = kConeWgsPerCu == 4 ? 192 : 384;          // rows per level (row-offset table, descriptors)
+constexpr int kDescEntries = kConeWgsPerCu == 4 ? 512 : 1024;     // row-descriptor table (all levels of a unit)
 constexpr int kMaxTileLevels = 6;           // L for tile items
 constexpr int kMaxLevels = 11;              // merge levels of any unit (whole units: ceil(log2(kMaxRows)))
 constexpr int kMaxRanges = (1 << (kMaxTileLevels + 1)) - 1;
@@ -62,7 +69,21 @@ constexpr int kMaxRowsPerWave = 24;         // merge: staged rows per wave
 // unit without one (a whole unit too large for the descriptor table) has
 // UnitDesc::pad = kNoBlob.  kCarriedRow: the tail-row field of a size-1 node
 // carried unchanged.
-constexpr int kBlobHeader = 32;
+constexpr int kBlobHeader = 48;
+// header words: rows of levels 0..L at [0, 12), first descriptor of each
+// level at [12, 24), then the counts, then the row-slot table of each merge
+// step's output level at [32, 44) (0: no table)
+enum : int {
+    kHdrRows = 0, kHdrDesc = 12, kHdrRuns = 24, kHdrEntries = 25, kHdrBottom = 26, kHdrSlotWords = 27,
+    kHdrRunOff = 28, kHdrSlotOff = 32
+};
+// row slots (merge steps of units with a blob, SMAX <= 5): a wave's register
+// rows 2q, 2q + 1 hold slot q: one row, two independent rows, or a row pair
+// r, r + 1 with the same head and tail rows and roll shifts s, s + 1 (the
+// second row's tail term is the first's shifted by one bin).  Slot word:
+// row A | row B << 10 | kind << 20.
+enum : uint32_t { kSlotOne = 0, kSlotTwo = 1, kSlotPair = 2 };
+constexpr int kSlotWords = kConeWgsPerCu == 4 ? 288 : 544;   // LDS area of a unit's slot tables
 constexpr uint32_t kNoBlob = 0xFFFFFFFFu;
 constexpr uint32_t kCarriedRow = 1023;
 // 16-byte chunks of a unit's LDS DMA fill (setup_unit): a whole unit's block
@@ -152,7 +173,7 @@ enum : uint8_t { kModeWhole = 0, kModeTile = 1 };
 // RT_STAMPS diagnostic builds: one record per work unit of kStampRecWords
 // words: hw id | xcc << 32, kStampMarks s_memtime marks (start, setup done,
 // fill issued, descriptors built, fill landed, merge done, end), shape bits.
-constexpr int kStampMarks = 11;   // + S/N pass 0: prefix, barrier, window, end
+constexpr int kStampMarks = 14;   // + S/N pass 0: prefix, barrier, window, end; + unit_begin: view, header, DMA issued
 constexpr int kStampRecWords = kStampMarks + 2;
 constexpr uint64_t kTimelineCap = 1u << 21;
 // cone kernel feature bits (ConeArgs::flags)
@@ -165,6 +186,7 @@ enum : uint32_t {
     kConeDiagNoBarrier = 1u << 27, // diagnostics only (wrong results): no barriers between merge levels
     kConeDiagNoLand = 1u << 26,  // diagnostics only (wrong results): fill loads issued but not landed in LDS
     kConeDiagNoDesc = 1u << 25,  // diagnostics only (wrong results): no descriptor table
+    kConeDiagExitWait = 1u << 24, // A/B only: wait for the unit's stores before the workgroup ends
     kConeDefaultFeatures = 3u
 };
 enum : uint8_t { kSelLeaves = 0, kSelPing = 1, kSelPong = 2, kSelSnr = 3 };
@@ -191,9 +213,13 @@ struct UnitDesc {
     float stdnoise;
     uint64_t src_off, buf_off, snr_row;
     uint8_t levels, mode, src, dst;
-    uint32_t pad;         // tile units: word offset of the unit's blob in ConeArgs::blob
+    uint32_t pad;         // word offset of the unit's blob in ConeArgs::blob (kNoBlob: none)
+    // the blob's header counts (kHdrRuns .. kHdrRunOff), so the kernel issues
+    // the unit's DMA after one scalar load instead of a dependent chain
+    uint32_t nruns, entries, nb, slot_words, run_off;
+    uint32_t pad2[3];
 };
-static_assert(sizeof(UnitDesc) == 64, "UnitDesc layout");
+static_assert(sizeof(UnitDesc) == 96, "UnitDesc layout");
 
 // Arguments of one cone-kernel launch.  Per-trial strides are in floats.
 struct ConeArgs {

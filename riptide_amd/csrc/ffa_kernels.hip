@@ -212,7 +212,8 @@ struct UnitView {
     int p, m, rows_eval;
     uint64_t src_off, buf_off, snr_row;
     float stdnoise;
-    uint32_t blob;            // tile units: word offset of the host-built blob
+    uint32_t blob;            // word offset of the host-built blob (kNoBlob: none)
+    int nruns, entries, nb, slot_words, run_off;   // its header counts
 };
 
 typedef const __attribute__((address_space(4))) uint32_t* const_u32_ptr;
@@ -246,25 +247,40 @@ __device__ __forceinline__ UnitView unit_view(const ConeArgs& a, int item, int t
     v.snr_row = uni64(d.snr_row);
     v.stdnoise = __int_as_float(uni(__float_as_int(d.stdnoise)));
     v.blob = (uint32_t)uni((int)d.pad);
+    v.nruns = uni((int)d.nruns);
+    v.entries = uni((int)d.entries);
+    v.nb = uni((int)d.nb);
+    v.slot_words = uni((int)d.slot_words);
+    v.run_off = uni((int)d.run_off);
     return v;
 }
 
 // Per-unit context (wave-uniform) and its LDS metadata: for tile units the
 // blob (kBlobHeader words of header, the DMA runs, the descriptor table, the
 // bottom-row offsets) DMA'd into `aux`.
-constexpr int kAuxWords = kBlobHeader + 4 * (1 << kMaxTileLevels) + kDescEntries + kMaxRows;
+constexpr int kAuxWords = kBlobHeader + kDescEntries + kMaxRows + kSlotWords;
 struct UnitCtx {
     UnitView U;
     bool tile;                // a tile unit (else: a whole node)
     bool table;               // the host-built blob is in aux (every tile unit, most whole units)
     int al;                   // whole units: 16-byte phase (floats) of the block
-    int nruns, entries, nb;   // tile units: header words 24..26
-    const uint32_t* aux;      // tile units: the blob in LDS
+    bool slots;               // the blob holds row-slot tables (merge_step_slots)
+    int nruns, entries, nb;   // blob header counts
+    const uint32_t* aux;      // the blob's LDS part in LDS
 };
 
-__device__ __forceinline__ int rows_at(const UnitCtx& C, int l) { return C.table ? uni((int)C.aux[l]) : C.U.node_size; }
-__device__ __forceinline__ int desc_offset(const UnitCtx& C, int l) { return uni((int)C.aux[12 + l]); }
-__device__ __forceinline__ const uint32_t* desc_table(const UnitCtx& C) { return C.aux + kBlobHeader + 4 * C.nruns; }
+__device__ __forceinline__ int rows_at(const UnitCtx& C, int l)
+{
+    return C.table ? uni((int)C.aux[kHdrRows + l]) : C.U.node_size;
+}
+__device__ __forceinline__ int desc_offset(const UnitCtx& C, int l) { return uni((int)C.aux[kHdrDesc + l]); }
+__device__ __forceinline__ const uint32_t* desc_table(const UnitCtx& C) { return C.aux + kBlobHeader; }
+// the row-slot table of the merge step whose output level is lo: its slot
+// count, then one word per slot
+__device__ __forceinline__ const uint32_t* slot_table(const UnitCtx& C, int lo)
+{
+    return C.aux + uni((int)C.aux[kHdrSlotOff + lo]);
+}
 __device__ __forceinline__ const int* bottom_offsets(const UnitCtx& C)
 {
     return reinterpret_cast<const int*>(desc_table(C) + C.entries);
@@ -302,12 +318,15 @@ __device__ __forceinline__ void dma_run(__amdgpu_buffer_rsrc_t rs, uint32_t goff
 // (unmasked full slots; kPack2: the p <= 32 rows).
 template <int SMAX, int RW>
 __device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t u, uint32_t* aux, float* buf, int tid,
-                                              bool dma, bool& ok)
+                                              bool dma, bool& ok, unsigned long long* ts = nullptr)
 {
     const int lane = tid & 63, wave = tid >> 6;
     UnitCtx C;
     C.U = unit_view(a, (int)(u / a.batch), (int)(u % a.batch));
     const UnitView& U = C.U;
+#ifdef RT_STAMPS
+    if (ts) ts[0] = __builtin_amdgcn_s_memtime() + (U.p & 0);
+#endif
     C.tile = U.mode == kModeTile;
     C.table = U.blob != kNoBlob;
     C.aux = aux;
@@ -323,31 +342,54 @@ __device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t u, uin
     const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(src, (((uint32_t)U.m * (uint32_t)p + 3u) & ~3u) * 4u);
     if (!C.table) {
         C.al = (int)(((uint32_t)U.node_start * (uint32_t)p) & 3u);
+        C.slots = false;
         C.nruns = C.entries = C.nb = 0;
         const int nch = (U.node_size * p + C.al + 3) >> 2;
         ok = ok && !C.tile && U.node_size <= cap && 4 * nch <= kLdsBufFloats;
+#ifdef RT_STAMPS
+        if (ts) ts[1] = __builtin_amdgcn_s_memtime();
+#endif
         if (ok && dma)
             dma_run(rs, ((uint32_t)U.node_start * (uint32_t)p - (uint32_t)C.al) * 4u, nch, buf, wave, kConeWaves, lane);
     } else {
         C.al = 0;
-        const const_u32_ptr blob = (const_u32_ptr)(uintptr_t)(a.blob + U.blob);
-        C.nruns = uni((int)blob[24]);
-        C.entries = uni((int)blob[25]);
-        C.nb = uni((int)blob[26]);
-        const int words = kBlobHeader + 4 * C.nruns + C.entries + C.nb;
-        ok = ok && C.nb <= cap && C.entries <= kDescEntries && words <= kAuxWords && C.nruns <= (1 << kMaxTileLevels);
+        // the blob's header counts come with the view (UnitDesc); its DMA
+        // runs with one vector load (lane i: run i) -- the unit's DMA is
+        // issued two memory round trips after the workgroup starts (a scalar
+        // load per run took ~10K cycles for a 16-run tile)
+        C.nruns = U.nruns;
+        C.entries = U.entries;
+        C.nb = U.nb;
+        C.slots = U.slot_words != 0;
+        const int words = U.run_off;   // the LDS part: header .. slot tables
+        ok = ok && C.nb <= cap && C.entries <= kDescEntries && words <= kAuxWords &&
+             words >= kBlobHeader + C.entries + C.nb && C.nruns <= 64 * kConeWaves && (words & 3) == 0;
+#ifdef RT_STAMPS
+        if (ts) ts[1] = __builtin_amdgcn_s_memtime() + (ok ? 0 : 0);
+#endif
         if (ok && dma) {
-            // the blob: the last wave; the runs: all waves, round-robin
-            const __amdgpu_buffer_rsrc_t rb = buffer_rsrc(a.blob + U.blob, (uint32_t)((words + 3) & ~3) * 4u);
-            if (wave == kConeWaves - 1) dma_run(rb, 0u, (words + 3) >> 2, (float*)aux, 0, 1, lane);
-            for (int ri = wave; ri < C.nruns; ri += kConeWaves) {
-                const uint32_t g = blob[kBlobHeader + 4 * ri];
-                const int cb = (int)blob[kBlobHeader + 4 * ri + 1];
-                const int nch = (int)blob[kBlobHeader + 4 * ri + 2];
-                if (4 * (cb + nch) <= kLdsBufFloats) dma_run(rs, g * 4u, nch, buf + 4 * cb, 0, 1, lane);
+            // DMA segments: wave w issues segments w, w + 8, ...; its lane i
+            // holds segment w + 8i (one vector load)
+            const uint4* const segs = reinterpret_cast<const uint4*>(a.blob + U.blob + words);
+            const int mine = uni(C.nruns > wave ? (C.nruns - wave + kConeWaves - 1) / kConeWaves : 0);
+            uint4 sv = make_uint4(0u, 0u, 0u, 0u);
+            if (lane < mine) sv = segs[wave + kConeWaves * lane];
+            // the blob's LDS part: the last wave
+            const __amdgpu_buffer_rsrc_t rb = buffer_rsrc(a.blob + U.blob, (uint32_t)words * 4u);
+            if (wave == kConeWaves - 1) dma_run(rb, 0u, words >> 2, (float*)aux, 0, 1, lane);
+            for (int i = 0; i < mine; ++i) {
+                const int c0 = __builtin_amdgcn_readlane((int)sv.x, i);
+                const int n = __builtin_amdgcn_readlane((int)sv.y, i);
+                const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)sv.z, i);
+                if (lane < n && 4 * (c0 + n) <= kLdsBufFloats)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(buf + 4 * c0),
+                                                             16, (int)((g + (uint32_t)lane) * 16u), 0, 0, 0);
             }
         }
     }
+#ifdef RT_STAMPS
+    if (ts) ts[2] = __builtin_amdgcn_s_memtime();
+#endif
     return C;
 }
 
@@ -416,6 +458,10 @@ typedef const __attribute__((address_space(3))) float* lds_cptr;
 // LDS reads the compiler must not pair into ds_read2_b32 / ds_read2st64_b32
 // (those issue at a lower rate than separate ds_read_b32 on gfx950,
 // tools/microbench/lds_b64.hip): volatile accesses are never merged.
+#ifndef RT_MERGE_PIPE
+#define RT_MERGE_PIPE 0
+#endif
+
 __device__ __forceinline__ float lds_ld(lds_cptr p) { return *(const volatile __attribute__((address_space(3))) float*)p; }
 
 // Outputs of level l (rows wave + 8i) into v, from the level below in dense
@@ -512,6 +558,46 @@ __device__ __forceinline__ void merge_level2_dense(const UnitCtx& C, const float
         s3 = sTT;
     }
     const lds_cptr l1 = (lds_cptr)src + lane;
+#if RT_MERGE_PIPE
+    if constexpr (SMAX <= 5) {
+        // software-pipelined rows: the reads of row i + 1 are issued before
+        // the additions of row i, so a wave keeps up to 4 SMAX LDS reads in
+        // flight across the row boundary instead of draining per row
+        float x[2][SMAX][4];
+        auto issue = [&](int i, float (&xx)[SMAX][4]) {
+            const lds_cptr hrow = l1 + __builtin_amdgcn_readlane(o0, i);
+            lds_cptr b1 = l1 + __builtin_amdgcn_readlane(o1, i);
+            lds_cptr b2 = l1 + __builtin_amdgcn_readlane(o2, i);
+            lds_cptr b3 = l1 + __builtin_amdgcn_readlane(o3, i);
+            lds_cptr w1 = b1 - p, w2 = b2 - p, w3 = b3 - p;
+            asm("" : "+v"(b1), "+v"(w1), "+v"(b2), "+v"(w2), "+v"(b3), "+v"(w3));
+            const int ls1 = lane + __builtin_amdgcn_readlane(s1, i);
+            const int ls2 = lane + __builtin_amdgcn_readlane(s2, i);
+            const int ls3 = lane + __builtin_amdgcn_readlane(s3, i);
+#pragma unroll
+            for (int k = 0; k < SMAX; ++k) {
+                const int wk = p - 64 * k;
+                xx[k][0] = hrow[64 * k];
+                xx[k][1] = lds_ld((ls1 >= wk ? w1 : b1) + 64 * k);
+                xx[k][2] = lds_ld((ls2 >= wk ? w2 : b2) + 64 * k);
+                xx[k][3] = lds_ld((ls3 >= wk ? w3 : b3) + 64 * k);
+            }
+        };
+        issue(0, x[0]);
+#pragma unroll
+        for (int i = 0; i < RW; ++i) {
+            if (i + 1 < RW) issue(i + 1, x[(i + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < SMAX; ++k) {
+                const float(&y)[4] = x[i & 1][k];
+                v[i][k] = __fadd_rn(__fadd_rn(y[0], y[1]), __fadd_rn(y[2], y[3]));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        return;
+    }
+#endif
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
         const lds_cptr hrow = l1 + __builtin_amdgcn_readlane(o0, i);
@@ -669,6 +755,187 @@ __device__ __forceinline__ void write_rows_packed(float* base, float* dummy, con
     }
 }
 
+// Row-slot merge steps (units with a blob, SMAX <= 5 rows of exactly SMAX
+// slots; common.hpp kSlotPair).  A wave's slot q fills register rows 2q and
+// 2q + 1: one output row, two independent rows, or a row pair r, r + 1 with
+// the same head and tail rows and roll shifts s, s + 1.  The pair's second
+// row reuses the first's terms: with H = the head term and T the rolled tail
+// term of row r (fused: H = HH + roll(HT, sH), T = roll(TH, s) +
+// roll(TT, s + sT)), row r + 1 is H[j] + T[(j + 1) mod p] -- the same float
+// operands in the same association as computing it directly, so bit-exact --
+// taken with one DPP lane shift (wave_shl:1) per 64-bin slot, the slot's
+// lane 63 from lane 0 of the next slot, and bin p - 1 from bin 0.  Half the
+// LDS reads of the pair.
+//
+// Per-row terms of the row whose resolved descriptor sits in lane i.
+template <int SMAX, bool TWO>
+__device__ __forceinline__ void row_terms(lds_cptr l1, int p, int lane, int i, int o0, int o1, int o2, int o3, int s1,
+                                          int s2, int s3, float (&hs)[SMAX], float (&ts)[SMAX])
+{
+    if constexpr (TWO) {
+        const lds_cptr hrow = l1 + __builtin_amdgcn_readlane(o0, i);
+        lds_cptr b1 = l1 + __builtin_amdgcn_readlane(o1, i);
+        lds_cptr b2 = l1 + __builtin_amdgcn_readlane(o2, i);
+        lds_cptr b3 = l1 + __builtin_amdgcn_readlane(o3, i);
+        lds_cptr w1 = b1 - p, w2 = b2 - p, w3 = b3 - p;
+        asm("" : "+v"(b1), "+v"(w1), "+v"(b2), "+v"(w2), "+v"(b3), "+v"(w3));
+        const int ls1 = lane + __builtin_amdgcn_readlane(s1, i);
+        const int ls2 = lane + __builtin_amdgcn_readlane(s2, i);
+        const int ls3 = lane + __builtin_amdgcn_readlane(s3, i);
+#pragma unroll
+        for (int k = 0; k < SMAX; ++k) {
+            const int wk = p - 64 * k;
+            const float x1 = lds_ld((ls1 >= wk ? w1 : b1) + 64 * k);
+            const float x2 = lds_ld((ls2 >= wk ? w2 : b2) + 64 * k);
+            const float x3 = lds_ld((ls3 >= wk ? w3 : b3) + 64 * k);
+            hs[k] = __fadd_rn(hrow[64 * k], x1);
+            ts[k] = __fadd_rn(x2, x3);
+        }
+    } else {
+        // o0 head row, o1 tail row + shift, s1 shift, o2 carried (size-1 node:
+        // the tail term is -0.0, x + (-0.0) == x exactly)
+        const lds_cptr hrow = l1 + __builtin_amdgcn_readlane(o0, i);
+        lds_cptr ta = l1 + __builtin_amdgcn_readlane(o1, i);
+        lds_cptr tw = ta - p;
+        asm("" : "+v"(ta), "+v"(tw));
+        const int ls = lane + __builtin_amdgcn_readlane(s1, i);
+        const uint32_t keep = __builtin_amdgcn_readlane(o2, i) ? 0u : 0xFFFFFFFFu;
+        const uint32_t neg0 = ~keep & 0x80000000u;
+#pragma unroll
+        for (int k = 0; k < SMAX; ++k) {
+            const float x = lds_ld((ls >= p - 64 * k ? tw : ta) + 64 * k);
+            hs[k] = hrow[64 * k];
+            ts[k] = __uint_as_float((__float_as_uint(x) & keep) | neg0);
+        }
+    }
+}
+
+template <int SMAX, int RW, bool TWO>
+__device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* src, int p, int lo, int lane,
+                                                 int wave, float (&v)[RW][SMAX], const int* loff, uint32_t& sw,
+                                                 int& nq)
+{
+    constexpr int Q = (RW + 1) / 2;
+    static_assert(Q <= 32, "row slots: one lane per slot row");
+    const uint32_t* st = slot_table(C, lo);
+    const int ns = uni((int)st[0]);
+    nq = uni(ns > wave ? (ns - wave + kConeWaves - 1) / kConeWaves : 0);
+    // lane i < 32 resolves row A of the wave's slot i, lane 32 + i its row B
+    const int qi = lane & 31;
+    sw = qi < nq ? st[1 + wave + kConeWaves * qi] : 0u;
+    const bool act = qi < nq && (lane < 32 || (sw >> 20) == kSlotTwo);
+    const int r = lane < 32 ? (int)(sw & 1023u) : (int)((sw >> 10) & 1023u);
+    const uint32_t* const desc = desc_table(C);
+    int o0 = 0, o1 = 0, o2 = 0, o3 = 0, s1 = 0, s2 = 0, s3 = 0;
+    if (act) {
+        if constexpr (TWO) {
+            const uint32_t d0 = desc[desc_offset(C, lo) + r];
+            const uint32_t dh = desc[desc_offset(C, lo + 1) + (int)(d0 & 1023u)];
+            const uint32_t dt = desc[desc_offset(C, lo + 1) + (int)((d0 >> 10) & 1023u)];
+            const int sh = (int)(d0 >> 20), sH = (int)(dh >> 20), sT = (int)(dt >> 20);
+            int sTT = sh + sT;
+            sTT = sTT >= p ? sTT - p : sTT;
+            const uint32_t r0 = dh & 1023u, r1 = (dh >> 10) & 1023u, r2 = dt & 1023u, r3 = (dt >> 10) & 1023u;
+            o0 = (loff ? loff[r0] : (int)r0 * p);
+            o1 = (loff ? loff[r1] : (int)r1 * p) + sH;
+            o2 = (loff ? loff[r2] : (int)r2 * p) + sh;
+            o3 = (loff ? loff[r3] : (int)r3 * p) + sTT;
+            s1 = sH;
+            s2 = sh;
+            s3 = sTT;
+        } else {
+            const uint32_t d = desc[desc_offset(C, lo) + r];
+            const uint32_t tc = (d >> 10) & 1023u;
+            s1 = (int)(d >> 20);
+            o0 = loff ? loff[d & 1023u] : (int)(d & 1023u) * p;
+            o1 = (tc == kCarried ? o0 : (loff ? loff[tc] : (int)tc * p)) + s1;
+            o2 = tc == kCarried;
+        }
+    }
+    const lds_cptr l1 = (lds_cptr)src + lane;
+    const int jl = p - 1 - 64 * (SMAX - 1);   // lane of bin p - 1 in the last slot
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        if (q < nq) {
+            const uint32_t kq = (uint32_t)__builtin_amdgcn_readlane((int)sw, q) >> 20;
+            float hs[SMAX], ts[SMAX];
+            row_terms<SMAX, TWO>(l1, p, lane, q, o0, o1, o2, o3, s1, s2, s3, hs, ts);
+#pragma unroll
+            for (int k = 0; k < SMAX; ++k) v[2 * q][k] = __fadd_rn(hs[k], ts[k]);
+            const int qb = 2 * q + 1 < RW ? 2 * q + 1 : RW - 1;   // row B's register row (q < Q: in range)
+            if (2 * q + 1 < RW) {
+                if (kq == kSlotPair) {
+                    const float t0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ts[0]), 0));
+#pragma unroll
+                    for (int k = 0; k < SMAX; ++k) {
+                        float x = __int_as_float(
+                            __builtin_amdgcn_update_dpp(0, __float_as_int(ts[k]), 0x130, 0xF, 0xF, false));
+                        if (k + 1 < SMAX) {
+                            const float n0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ts[k + 1]), 0));
+                            x = lane == 63 ? n0 : x;
+                        } else {
+                            x = lane == jl ? t0 : x;
+                        }
+                        v[qb][k] = __fadd_rn(hs[k], x);
+                    }
+                } else if (kq == kSlotTwo) {
+                    row_terms<SMAX, TWO>(l1, p, lane, 32 + q, o0, o1, o2, o3, s1, s2, s3, hs, ts);
+#pragma unroll
+                    for (int k = 0; k < SMAX; ++k) v[qb][k] = __fadd_rn(hs[k], ts[k]);
+                }
+            }
+        }
+    }
+}
+
+// Slot-step write-back into the dense LDS rows at base / store to global
+// memory (a non-final pass's output level): register rows 2q, 2q + 1 to the
+// slot's rows A and B.
+template <int SMAX, int RW>
+__device__ __forceinline__ void write_rows_slots(float* base, float* dummy, const float (&v)[RW][SMAX], int p,
+                                                 int lane, uint32_t sw, int nq)
+{
+    const bool tail_ok = lane + 64 * (SMAX - 1) < p;
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+        if (i / 2 < nq) {
+            const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)sw, i / 2);
+            if (i % 2 == 0 || (w >> 20) != kSlotOne) {
+                const int row = (int)((i % 2 == 0 ? w : w >> 10) & 1023u);
+                float* orow = base + row * p + lane;
+#pragma unroll
+                for (int k = 0; k < SMAX; ++k) {
+                    if (k < SMAX - 1) orow[64 * k] = v[i][k];
+                    else *(tail_ok ? orow + 64 * k : dummy) = v[i][k];
+                }
+            }
+        }
+    }
+}
+
+template <int SMAX, int RW>
+__device__ __forceinline__ void store_rows_slots(const float (&v)[RW][SMAX], int p, int lane, uint32_t sw, int nq,
+                                                 __amdgpu_buffer_rsrc_t rs, uint32_t st_o0)
+{
+    const bool tail_ok = lane + 64 * (SMAX - 1) < p;
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+        if (i / 2 < nq) {
+            const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)sw, i / 2);
+            if (i % 2 == 0 || (w >> 20) != kSlotOne) {
+                const int row = (int)((i % 2 == 0 ? w : w >> 10) & 1023u);
+                const uint32_t ob = st_o0 + (uint32_t)(row * p + lane) * 4u;
+#pragma unroll
+                for (int k = 0; k < SMAX; ++k) {
+                    const uint32_t o = k < SMAX - 1 ? ob + 256u * (uint32_t)k
+                                                    : (tail_ok ? ob + 256u * (uint32_t)k : 0x80000000u);
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs, (int)o, 0, 0);
+                }
+            }
+        }
+    }
+}
+
 // All merge levels of one unit, deepest first, in place in the dense rows
 // at `base`.  SMAX >= ceil(p/64) slots per row, RW rows per wave
 // (lds_row_capacity(p, SMAX) guarantees ceil(rows/8) <= RW at every level).
@@ -692,6 +959,32 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
     // below the step's output holds size-1 nodes, single steps before that
     // and for a last odd level
     const bool fuse = (flags & kConeFuse2) && SMAX != kPack2;
+    if constexpr (SMAX <= 5) {
+        if (C.slots && fuse) {
+            // row-slot steps (the host's slot tables follow this step order)
+            for (int l = L - 1; l >= 0;) {
+                const bool two = l >= 1 && (tile || (node_size >> l) >= 2);
+                const int lo = two ? l - 1 : l;
+                float v[RW][SMAX];
+                const bool first = l == L - 1;
+                const float* src = first ? src0 : base;
+                const int* lo_src = first ? loff : nullptr;
+                uint32_t sw;
+                int nq;
+                if (two) merge_step_slots<SMAX, RW, true>(C, src, p, lo, lane, wave, v, lo_src, sw, nq);
+                else merge_step_slots<SMAX, RW, false>(C, src, p, lo, lane, wave, v, lo_src, sw, nq);
+                l = lo - 1;
+                if (lo == 0 && st) {
+                    store_rows_slots<SMAX, RW>(v, p, lane, sw, nq, rs, st_o0);
+                    return;
+                }
+                if (!(flags & kConeDiagNoBarrier)) lds_barrier();
+                if (!(flags & kConeDiagNoWrite)) write_rows_slots<SMAX, RW>(base, dummy, v, p, lane, sw, nq);
+                if (!(flags & kConeDiagNoBarrier)) lds_barrier();
+            }
+            return;
+        }
+    }
     for (int l = L - 1; l >= 0;) {
         // size-1 nodes exist at depth l only in whole units with node_size >> l < 2
         const bool two = fuse && l >= 1 && (tile || (node_size >> l) >= 2);
@@ -1148,6 +1441,10 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
     __shared__ float whb[2 * kMaxWidths];   // S/N: h + b and b per width
 
     const int tid = threadIdx.x;
+#ifdef RT_STAMPS
+    const unsigned long long t_entry = __builtin_amdgcn_s_memtime();
+    unsigned long long t_begin[3] = {};
+#endif
     const uint32_t total = a.num_items * a.batch;
     uint32_t u = blockIdx.x;
     if (u >= total) return;
@@ -1155,7 +1452,11 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
     const bool dma = !(a.flags & kConeDiagNoLand);
     int b = 0;
     bool ok;
+#ifdef RT_STAMPS
+    UnitCtx C = unit_begin<SMAX, RW>(a, u, aux[0], data[0], tid, dma, ok, t_begin);
+#else
     UnitCtx C = unit_begin<SMAX, RW>(a, u, aux[0], data[0], tid, dma, ok);
+#endif
     for (;;) {
 #ifdef RT_STAMPS
         unsigned long long tl[kStampMarks] = {};
@@ -1213,8 +1514,14 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
         }
         lds_barrier();                        // the level buffer is free
 #ifdef RT_STAMPS
+        RT_MARK(4);
+        tl[5] = t_entry;
+        tl[11] = t_begin[0];
+        tl[12] = t_begin[1];
+        tl[13] = t_begin[2];
+        if (kConeBuffers == 1 && (a.flags & kConeDiagExitWait)) __builtin_amdgcn_s_waitcnt(0x0F70);
+        RT_MARK(6);
         if (tid == 0 && a.stamps) {
-            RT_MARK(4);
             unsigned long long* e = a.stamps + (uint64_t)kStampRecWords * (uint64_t)u;
             const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));     // HW_REG_HW_ID
             const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11));   // HW_REG_XCC_ID
@@ -1236,7 +1543,10 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
             C = unit_begin<SMAX, RW>(a, u, aux[0], data[0], tid, dma, ok);
         }
     }
-    __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0): no DMA outstanding at exit
+    // two buffers: no DMA outstanding at exit (LDS DMA into a freed
+    // allocation); one buffer: every DMA was waited for at the unit start,
+    // and the unit's global stores need no wait before the end of the program
+    if (kConeBuffers == 2 || (a.flags & kConeDiagExitWait)) __builtin_amdgcn_s_waitcnt(0x0F70);
 }
 
 // Persistent grid: kConeWgsPerCu workgroups per CU (RIPTIDE_AMD_CONE_PERSIST=0:

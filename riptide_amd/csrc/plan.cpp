@@ -397,7 +397,14 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
     }
     // host-built metadata of the tile items (trial-independent, shared by a
     // launch's whole batch)
-    for (ConeItem& it : out.items) {
+    std::vector<int> slot_rw(out.items.size(), 0);
+    for (const Launch& L : out.launches) {
+        // row-slot tables for the kernel instances that use them (SMAX <= 5)
+        const int rw = L.smax <= 5 ? (L.rw ? (int)L.rw : merge_rows_per_wave((int)L.smax)) : 0;
+        for (uint32_t i = L.first; i < L.first + L.count; ++i) slot_rw[i] = rw;
+    }
+    for (size_t i = 0; i < out.items.size(); ++i) {
+        ConeItem& it = out.items[i];
         it.pad = kNoBlob;
         // whole units: a descriptor table only when it fits the LDS area
         // (otherwise the kernel derives the node partition on the fly)
@@ -405,12 +412,68 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
             ((uint64_t)it.levels * it.node_size > (uint64_t)kDescEntries || it.node_size > (uint32_t)kMaxRows))
             continue;
         it.pad = (uint32_t)out.blob.size();
-        build_tile_blob(it, out.xf[it.xform].p, out.blob);
+        build_tile_blob(it, out.xf[it.xform].p, slot_rw[i], out.blob);
     }
     validate_exec_plan(out, snr_epilogue);
 }
 
-void build_tile_blob(const ConeItem& it, uint32_t p, std::vector<uint32_t>& out)
+// Row slots of one merge step (output level with n rows, descriptors d):
+// rows in order, a pair where rows r, r + 1 share head and tail rows with
+// shifts s, s + 1 (never carried rows), filled into the slots g = wave + 8q
+// of the wave's register rows 2q, 2q + 1 (capacity 2, or 1 for the last
+// slot of an odd RW).  Every slot is filled to its capacity (a pair split
+// into two rows where needed), so n <= 8 RW rows always fit.
+static void build_row_slots(const uint32_t* d, uint32_t n, uint32_t p, int rw, std::vector<uint32_t>& slots)
+{
+    struct Item { uint32_t r; bool pair; };
+    std::vector<Item> items;
+    for (uint32_t r = 0; r < n;) {
+        const uint32_t a = d[r];
+        if (r + 1 < n && ((a ^ d[r + 1]) & 0xFFFFFu) == 0 && ((a >> 10) & 1023u) != kCarriedRow &&
+            (d[r + 1] >> 20) == ((a >> 20) + 1) % p) {
+            items.push_back({r, true});
+            r += 2;
+        } else {
+            items.push_back({r, false});
+            r += 1;
+        }
+    }
+    const int Q = (rw + 1) / 2;
+    slots.clear();
+    size_t c = 0;
+    for (int g = 0; c < items.size(); ++g) {
+        if (g >= kConeWaves * Q) throw std::runtime_error("schedule: merge level exceeds the register rows");
+        const int cap = (g / kConeWaves == Q - 1 && (rw & 1)) ? 1 : 2;
+        Item& A = items[c];
+        if (A.pair && cap == 2) {
+            slots.push_back(A.r | ((A.r + 1) << 10) | (kSlotPair << 20));
+            ++c;
+            continue;
+        }
+        const uint32_t ra = A.r;
+        if (A.pair) {            // split: row A alone, its partner stays next
+            A.r += 1;
+            A.pair = false;
+        } else {
+            ++c;
+        }
+        if (cap == 1 || c == items.size()) {
+            slots.push_back(ra | (kSlotOne << 20));
+            continue;
+        }
+        Item& B = items[c];
+        const uint32_t rb = B.r;
+        if (B.pair) {
+            B.r += 1;
+            B.pair = false;
+        } else {
+            ++c;
+        }
+        slots.push_back(ra | (rb << 10) | (kSlotTwo << 20));
+    }
+}
+
+void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, std::vector<uint32_t>& out)
 {
     struct R { uint32_t size, lo, hi; uint32_t start; uint32_t base; };
     const int L = it.levels;
@@ -447,19 +510,11 @@ void build_tile_blob(const ConeItem& it, uint32_t p, std::vector<uint32_t>& out)
     }
     const size_t o = out.size();
     const uint32_t nruns = (uint32_t)lv[L].size(), nb = nrows[L];
-    const size_t words = kBlobHeader + 4 * (size_t)nruns + entries + nb;
-    out.resize(o + ((words + 3) & ~(size_t)3), 0u);
-    uint32_t* w = out.data() + o;
-    for (int l = 0; l <= L; ++l) {
-        w[l] = nrows[l];
-        w[12 + l] = doff[l];
-    }
-    w[24] = nruns;
-    w[25] = entries;
-    w[26] = nb;
-    uint32_t* run = w + kBlobHeader;
-    uint32_t* desc = run + 4 * nruns;
-    uint32_t* loff = desc + entries;
+    // [header | descriptors | bottom-row offsets | row slots] goes to LDS;
+    // the DMA runs behind them are read by the kernel's scalar loads only.
+    // The descriptor table is filled first, the slot tables after it.
+    std::vector<uint32_t> desc_v(entries);
+    uint32_t* desc = desc_v.data();
     for (int l = 0; l < L; ++l) {
         if (!tile) {
             // whole unit (cone_kernel row_desc): row r of depth l lies in the
@@ -504,19 +559,63 @@ void build_tile_blob(const ConeItem& it, uint32_t p, std::vector<uint32_t>& out)
             desc[doff[l] + r] = h | (t << 10) | (sh << 20);
         }
     }
-    // bottom level: one DMA run per range, each at its own 16-byte phase
+    // row slots of every merge step (the kernel's step order: two levels per
+    // step where no level below the output holds size-1 nodes)
+    std::vector<uint32_t> slot_area;
+    uint32_t slot_off[kMaxLevels + 1] = {};
+    if (slot_rw > 0) {
+        std::vector<uint32_t> sl;
+        for (int l = L - 1; l >= 0;) {
+            const bool two = l >= 1 && (tile || (it.node_size >> l) >= 2);
+            const int lo = two ? l - 1 : l;
+            build_row_slots(desc + doff[lo], nrows[lo], p, slot_rw, sl);
+            slot_off[lo] = (uint32_t)(kBlobHeader + entries + nb + slot_area.size());
+            slot_area.push_back((uint32_t)sl.size());
+            slot_area.insert(slot_area.end(), sl.begin(), sl.end());
+            l = lo - 1;
+        }
+        if (slot_area.size() > (size_t)kSlotWords) throw std::runtime_error("schedule: row-slot tables exceed their LDS area");
+    }
+    // bottom level: one DMA run per range, each at its own 16-byte phase,
+    // consecutive in LDS; issued as segments of <= 64 16-byte chunks (one
+    // LDS-DMA wave instruction each: LDS chunk c0, chunks n, source chunk g)
+    std::vector<uint32_t> loff_v(nb), segs;
     uint32_t cb = 0;
     for (uint32_t ri = 0; ri < nruns; ++ri) {
         const R& g = lv[L][ri];
         const uint32_t first = (g.start + g.lo) * p;
         const uint32_t al = first & 3u, cnt = g.hi - g.lo + 1;
         const uint32_t nch = (cnt * p + al + 3) >> 2;
-        run[4 * ri] = first - al;
-        run[4 * ri + 1] = cb;
-        run[4 * ri + 2] = nch;
-        for (uint32_t r = 0; r < cnt; ++r) loff[g.base + r] = 4 * cb + al + r * p;
+        for (uint32_t r = 0; r < cnt; ++r) loff_v[g.base + r] = 4 * cb + al + r * p;
+        for (uint32_t c = 0; c < nch; c += 64) {
+            segs.push_back(cb + c);
+            segs.push_back(std::min<uint32_t>(64u, nch - c));
+            segs.push_back((first - al) / 4 + c);
+            segs.push_back(0u);
+        }
         cb += nch;
     }
+    const uint32_t nsegs = (uint32_t)(segs.size() / 4);
+    if (nsegs > (uint32_t)(kConeWaves * 64)) throw std::runtime_error("schedule: unit fill exceeds the DMA segment table");
+    const size_t lds_words = kBlobHeader + entries + nb + slot_area.size();
+    const size_t runoff = (lds_words + 3) & ~(size_t)3;
+    const size_t words = runoff + segs.size();
+    out.resize(o + ((words + 3) & ~(size_t)3), 0u);
+    uint32_t* w = out.data() + o;
+    for (int l = 0; l <= L; ++l) {
+        w[kHdrRows + l] = nrows[l];
+        w[kHdrDesc + l] = doff[l];
+        w[kHdrSlotOff + l] = slot_off[l];
+    }
+    w[kHdrRuns] = nsegs;
+    w[kHdrEntries] = entries;
+    w[kHdrBottom] = nb;
+    w[kHdrSlotWords] = (uint32_t)slot_area.size();
+    w[kHdrRunOff] = (uint32_t)runoff;
+    std::copy(desc_v.begin(), desc_v.end(), w + kBlobHeader);
+    std::copy(loff_v.begin(), loff_v.end(), w + kBlobHeader + entries);
+    std::copy(slot_area.begin(), slot_area.end(), w + kBlobHeader + entries + nb);
+    std::copy(segs.begin(), segs.end(), w + runoff);
 }
 
 void validate_exec_plan(const ExecPlan& ex, bool snr_epilogue)

@@ -71,14 +71,19 @@ struct ExecPlan {
 // it, never recomputes it): the dependency cone's range tree flattened into
 // rows per level, the row-descriptor table of every level (head row | tail
 // row << 10 | roll shift << 20, transforms.hpp:13-27 restated per row), the
-// LDS DMA runs of the bottom level and the LDS float offset of every bottom
-// row in that fill layout.  Blob layout (uint32 words, 16-byte aligned):
+// LDS float offset of every bottom row in the fill layout, the row-slot table
+// of every merge step (slot_rw > 0: the launch's register rows per wave, see
+// kSlotPair) and the LDS DMA segments of the bottom level.  Blob layout
+// (uint32 words, 16-byte aligned; common.hpp kHdr*):
 //   [0, 12)  rows of levels 0..L        [12, 24) first descriptor of each level
-//   [24] runs  [25] descriptor entries  [26] bottom rows  [27, 32) 0
-//   [32, 32 + 4 runs)  per run: first float of the run in the transform block
-//                      (16-byte aligned), first chunk, chunks, 0
-//   then the descriptor table (entries words), then the bottom-row offsets.
-void build_tile_blob(const ConeItem& it, uint32_t p, std::vector<uint32_t>& out);
+//   [24] DMA segments  [25] descriptor entries  [26] bottom rows  [27] slot words
+//   [28] word offset of the segments    [32, 44) slot table of each level (0: none)
+//   [48, ...) descriptor table (entries words), bottom-row offsets, slot
+//             tables (each: slots, then one word per slot)  -- the LDS part
+//   [segments offset, + 4 segments)  per segment (one LDS-DMA wave
+//             instruction): first LDS chunk, chunks (<= 64), first source
+//             chunk (16 bytes) in the transform block, 0
+void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, std::vector<uint32_t>& out);
 
 // Schedule a list of transforms (p, m, rows_eval, src_off, snr_row, stdnoise
 // filled in by the caller).  With snr_epilogue the last pass of every

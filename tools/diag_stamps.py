@@ -19,7 +19,7 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
-MARKS = 11
+MARKS = 14
 REC = MARKS + 2
 PHASES = ["wait", "begin_next", "merge", "tail"]
 
@@ -64,6 +64,18 @@ def analyse(e):
     out = {"units": int(e.shape[0]), "distinct_cus": int(np.unique(cu).size),
            "mean_cycles": dict(zip(PHASES, ph.mean(axis=0).round(0).tolist())),
            "mean_total": float((tend - t[:, 0]).mean())}
+    # workgroup entry (mark 5) .. unit start (mark 0): prologue, view, blob
+    # header and DMA issue; mark 4 .. mark 6: the end-of-unit wait, if any
+    has_entry = bool(np.all(t[:, 5] > 0))
+    if has_entry:
+        out["mean_cycles"]["startup"] = float((t[:, 0] - t[:, 5]).mean())
+        out["mean_cycles"]["exit"] = float((t[:, 6] - tend).mean())
+        out["mean_total_entry_to_exit"] = float((t[:, 6] - t[:, 5]).mean())
+        if np.all(t[:, 11:14] > 0):
+            out["startup_split"] = {"view": float((t[:, 11] - t[:, 5]).mean()),
+                                    "header": float((t[:, 12] - t[:, 11]).mean()),
+                                    "dma_issue": float((t[:, 13] - t[:, 12]).mean()),
+                                    "rest": float((t[:, 0] - t[:, 13]).mean())}
     groups = {}
     for km in (0, 1):
         for ks in (0, 1):
@@ -72,6 +84,10 @@ def analyse(e):
                 g = {"units": int(m.sum()), "levels": round(float(lv[m].mean()), 2),
                      "rows": round(float(n0[m].mean()), 1)}
                 g.update(dict(zip(PHASES, ph[m].mean(axis=0).round(0).tolist())))
+                if np.all(t[:, 11:14] > 0):
+                    g["startup_split"] = {"view": round(float((t[m, 11] - t[m, 5]).mean())),
+                                          "header": round(float((t[m, 12] - t[m, 11]).mean())),
+                                          "dma_issue": round(float((t[m, 13] - t[m, 12]).mean()))}
                 groups[("whole" if km == 0 else "tile") + ("_snr" if ks else "")] = g
     out["groups"] = groups
     m = (snr == 1) & np.all(t[:, 7:11] > 0, axis=1)
@@ -83,9 +99,11 @@ def analyse(e):
     # per-CU residency and idle gaps (s_memtime is per XCD: compare within a CU only)
     occ = np.zeros(4)
     gaps = []
+    t_in = t[:, 5] if has_entry else t[:, 0]
+    t_out = t[:, 6] if has_entry else tend
     for c in np.unique(cu):
         m = cu == c
-        ev = np.concatenate([np.stack([t[m, 0], np.ones(m.sum())], 1), np.stack([tend[m], -np.ones(m.sum())], 1)])
+        ev = np.concatenate([np.stack([t_in[m], np.ones(m.sum())], 1), np.stack([t_out[m], -np.ones(m.sum())], 1)])
         ev = ev[np.lexsort((-ev[:, 1], ev[:, 0]))]
         level, last, idle_from = 0, ev[0, 0], None
         for tt, d in ev:

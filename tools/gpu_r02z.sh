@@ -1,0 +1,5 @@
+set -o pipefail
+mkdir -p gpurun_out/r02z
+bash tools/gpu_ab.sh r02z 3 || exit 1
+RIPTIDE_AMD_SCRATCH_MFLOATS=384 RIPTIDE_AMD_LIB=riptide_amd/libriptide_amd_stamps.so timeout -k 10 200 python -u tools/diag_stamps.py 4 > gpurun_out/r02z/stamps.json 2>gpurun_out/r02z/stamps.err || { tail -5 gpurun_out/r02z/stamps.err; exit 1; }
+cat gpurun_out/r02z/stamps.json
