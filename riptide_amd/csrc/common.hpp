@@ -187,6 +187,7 @@ enum : uint32_t {
     kConeDiagNoLand = 1u << 26,  // diagnostics only (wrong results): fill loads issued but not landed in LDS
     kConeDiagNoDesc = 1u << 25,  // diagnostics only (wrong results): no descriptor table
     kConeDiagExitWait = 1u << 24, // A/B only: wait for the unit's stores before the workgroup ends
+    kConeDiagNoFill = 1u << 23,  // diagnostics only (wrong results): metadata DMA only, no bottom-level fill
     kConeDefaultFeatures = 3u
 };
 enum : uint8_t { kSelLeaves = 0, kSelPing = 1, kSelPong = 2, kSelSnr = 3 };

@@ -381,7 +381,7 @@ __device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t u, uin
                 const int c0 = __builtin_amdgcn_readlane((int)sv.x, i);
                 const int n = __builtin_amdgcn_readlane((int)sv.y, i);
                 const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)sv.z, i);
-                if (lane < n && 4 * (c0 + n) <= kLdsBufFloats)
+                if (lane < n && 4 * (c0 + n) <= kLdsBufFloats && !(a.flags & kConeDiagNoFill))
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(buf + 4 * c0),
                                                              16, (int)((g + (uint32_t)lane) * 16u), 0, 0, 0);
             }
@@ -772,39 +772,49 @@ template <int SMAX, bool TWO>
 __device__ __forceinline__ void row_terms(lds_cptr l1, int p, int lane, int i, int o0, int o1, int o2, int o3, int s1,
                                           int s2, int s3, float (&hs)[SMAX], float (&ts)[SMAX])
 {
+    // all of the row's scalars first, in distinct SGPRs: a v_readlane result
+    // read by the next VALU instruction costs s_nop wait states
     if constexpr (TWO) {
-        const lds_cptr hrow = l1 + __builtin_amdgcn_readlane(o0, i);
-        lds_cptr b1 = l1 + __builtin_amdgcn_readlane(o1, i);
-        lds_cptr b2 = l1 + __builtin_amdgcn_readlane(o2, i);
-        lds_cptr b3 = l1 + __builtin_amdgcn_readlane(o3, i);
+        int r0 = __builtin_amdgcn_readlane(o0, i), r1 = __builtin_amdgcn_readlane(o1, i);
+        int r2 = __builtin_amdgcn_readlane(o2, i), r3 = __builtin_amdgcn_readlane(o3, i);
+        int t1 = __builtin_amdgcn_readlane(s1, i), t2 = __builtin_amdgcn_readlane(s2, i);
+        int t3 = __builtin_amdgcn_readlane(s3, i);
+        asm volatile("" : "+s"(r0), "+s"(r1), "+s"(r2), "+s"(r3), "+s"(t1), "+s"(t2), "+s"(t3));
+        const lds_cptr hrow = l1 + r0;
+        lds_cptr b1 = l1 + r1;
+        lds_cptr b2 = l1 + r2;
+        lds_cptr b3 = l1 + r3;
         lds_cptr w1 = b1 - p, w2 = b2 - p, w3 = b3 - p;
         asm("" : "+v"(b1), "+v"(w1), "+v"(b2), "+v"(w2), "+v"(b3), "+v"(w3));
-        const int ls1 = lane + __builtin_amdgcn_readlane(s1, i);
-        const int ls2 = lane + __builtin_amdgcn_readlane(s2, i);
-        const int ls3 = lane + __builtin_amdgcn_readlane(s3, i);
+        const int ls1 = lane + t1;
+        const int ls2 = lane + t2;
+        const int ls3 = lane + t3;
 #pragma unroll
         for (int k = 0; k < SMAX; ++k) {
             const int wk = p - 64 * k;
             const float x1 = lds_ld((ls1 >= wk ? w1 : b1) + 64 * k);
             const float x2 = lds_ld((ls2 >= wk ? w2 : b2) + 64 * k);
             const float x3 = lds_ld((ls3 >= wk ? w3 : b3) + 64 * k);
-            hs[k] = __fadd_rn(hrow[64 * k], x1);
+            hs[k] = __fadd_rn(lds_ld(hrow + 64 * k), x1);
             ts[k] = __fadd_rn(x2, x3);
         }
     } else {
         // o0 head row, o1 tail row + shift, s1 shift, o2 carried (size-1 node:
         // the tail term is -0.0, x + (-0.0) == x exactly)
-        const lds_cptr hrow = l1 + __builtin_amdgcn_readlane(o0, i);
-        lds_cptr ta = l1 + __builtin_amdgcn_readlane(o1, i);
+        int r0 = __builtin_amdgcn_readlane(o0, i), r1 = __builtin_amdgcn_readlane(o1, i);
+        int t1 = __builtin_amdgcn_readlane(s1, i), c1 = __builtin_amdgcn_readlane(o2, i);
+        asm volatile("" : "+s"(r0), "+s"(r1), "+s"(t1), "+s"(c1));
+        const lds_cptr hrow = l1 + r0;
+        lds_cptr ta = l1 + r1;
         lds_cptr tw = ta - p;
         asm("" : "+v"(ta), "+v"(tw));
-        const int ls = lane + __builtin_amdgcn_readlane(s1, i);
-        const uint32_t keep = __builtin_amdgcn_readlane(o2, i) ? 0u : 0xFFFFFFFFu;
+        const int ls = lane + t1;
+        const uint32_t keep = c1 ? 0u : 0xFFFFFFFFu;
         const uint32_t neg0 = ~keep & 0x80000000u;
 #pragma unroll
         for (int k = 0; k < SMAX; ++k) {
             const float x = lds_ld((ls >= p - 64 * k ? tw : ta) + 64 * k);
-            hs[k] = hrow[64 * k];
+            hs[k] = lds_ld(hrow + 64 * k);
             ts[k] = __uint_as_float((__float_as_uint(x) & keep) | neg0);
         }
     }
@@ -865,17 +875,14 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
             const int qb = 2 * q + 1 < RW ? 2 * q + 1 : RW - 1;   // row B's register row (q < Q: in range)
             if (2 * q + 1 < RW) {
                 if (kq == kSlotPair) {
-                    const float t0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ts[0]), 0));
+                    int n0[SMAX];
+#pragma unroll
+                    for (int k = 0; k < SMAX; ++k) n0[k] = __builtin_amdgcn_readlane(__float_as_int(ts[(k + 1) % SMAX]), 0);
 #pragma unroll
                     for (int k = 0; k < SMAX; ++k) {
-                        float x = __int_as_float(
-                            __builtin_amdgcn_update_dpp(0, __float_as_int(ts[k]), 0x130, 0xF, 0xF, false));
-                        if (k + 1 < SMAX) {
-                            const float n0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ts[k + 1]), 0));
-                            x = lane == 63 ? n0 : x;
-                        } else {
-                            x = lane == jl ? t0 : x;
-                        }
+                        // wave_shl:1 -- lane L takes lane L + 1 (lane 63: bound_ctrl 0, replaced)
+                        float x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(ts[k]), 0x130, 0xF, 0xF, true));
+                        x = lane == (k + 1 < SMAX ? 63 : jl) ? __int_as_float(n0[k]) : x;
                         v[qb][k] = __fadd_rn(hs[k], x);
                     }
                 } else if (kq == kSlotTwo) {
