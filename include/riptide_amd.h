@@ -112,6 +112,11 @@ int rt_schedule_check(size_t size, double tsamp, size_t num_widths, double perio
                       uint64_t* launches, double* alg_bytes_per_trial, double* moved_bytes_per_trial,
                       uint64_t* cells_per_trial);
 
+/* The pass schedule rt_ffa2 runs for one rows x cols transform, built and
+ * validated on the host only (validate_exec_plan: tiles, LDS budgets, unit
+ * blobs, DMA segments, row slots); no device needed.  *launches may be NULL. */
+int rt_ffa_schedule_check(size_t rows, size_t cols, uint64_t* launches);
+
 /* ------------------ device-resident batched hot path ---------------------- */
 
 typedef struct rt_plan rt_plan;

@@ -44,6 +44,7 @@ _SIGNATURES = {
     "rt_fast_running_median": (_c_i, [_vp, _c_sz, _c_sz, _c_sz, _vp]),
     "rt_deredden_normalise": (_c_i, [_vp, _c_sz, _c_sz, _c_sz, _c_i, _c_i, _vp]),
     "rt_periodogram_grid": (_c_i, [_c_sz, _c_d, _c_d, _c_d, _c_sz, _c_sz, _vp, _vp]),
+    "rt_ffa_schedule_check": (_c_i, [_c_sz, _c_sz, _pu64]),
     "rt_schedule_check": (_c_i, [_c_sz, _c_d, _c_sz, _c_d, _c_d, _c_sz, _c_sz, _pu64, _pu64, _pu64, _pd, _pd,
                                  _pu64]),
     "rt_plan_create": (_c_i, [_c_sz, _c_d, _vp, _c_sz, _c_d, _c_d, _c_sz, _c_sz, _vp]),

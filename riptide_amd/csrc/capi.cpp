@@ -194,6 +194,7 @@ struct DevicePlan {
                 d.nb = h[kHdrBottom];
                 d.slot_words = h[kHdrSlotWords];
                 d.run_off = h[kHdrRunOff];
+                d.fill_chunks = h[kHdrFill];
             }
             u[i] = d;
         }
@@ -888,6 +889,22 @@ int rt_periodogram_grid(size_t size, double tsamp, double pmin, double pmax, siz
         PgramPlan pg;
         build_pgram_plan(prm, pg);
         fill_grid(pg, periods, foldbins);
+        return RT_OK;
+    });
+}
+
+int rt_ffa_schedule_check(size_t rows, size_t cols, uint64_t* launches)
+{
+    return guarded([&] {
+        if (!rows || !cols || rows > 0xFFFFFFFFull || cols > 0xFFFFFFFFull || !merge_slots((uint32_t)cols))
+            throw std::invalid_argument("rt_ffa_schedule_check: bad shape");
+        FfaXform X{};
+        X.p = (uint32_t)cols;
+        X.m = (uint32_t)rows;
+        X.rows_eval = (uint32_t)rows;
+        ExecPlan ex;
+        build_exec_plan({X}, false, 0, ~0ull, ex);   // validates
+        if (launches) *launches = ex.launches.size();
         return RT_OK;
     });
 }

@@ -75,7 +75,7 @@ constexpr int kBlobHeader = 48;
 // step's output level at [32, 44) (0: no table)
 enum : int {
     kHdrRows = 0, kHdrDesc = 12, kHdrRuns = 24, kHdrEntries = 25, kHdrBottom = 26, kHdrSlotWords = 27,
-    kHdrRunOff = 28, kHdrSlotOff = 32
+    kHdrRunOff = 28, kHdrFill = 29, kHdrSlotOff = 32
 };
 // row slots (merge steps of units with a blob, SMAX <= 5): a wave's register
 // rows 2q, 2q + 1 hold slot q: one row, two independent rows, or a row pair
@@ -90,13 +90,19 @@ constexpr uint32_t kCarriedRow = 1023;
 // of n*p floats at 16-byte phase <= 3, or a tile's ranges, each a run at its
 // own phase (<= 2^L runs); the planner keeps every unit within a buffer.
 RT_HD inline int fill_chunks_bound(int n, int p, int runs) { return (n * p + 6 * runs + 3) >> 2; }
+// Units of the kPack2 variant (p <= 32: short rows leave most of the level
+// buffer free) keep their blob's LDS part (header, descriptors, bottom-row
+// offsets; no slot tables) at the end of their own level buffer instead of
+// the fixed metadata area, so the descriptor table may hold every level of
+// a 384-row unit.
+RT_HD inline int pack_blob_words(int entries, int nb) { return (kBlobHeader + entries + nb + 3) & ~3; }
 
 // Merge variant for rows of p phase bins: slots per row rounded up to an
 // instantiated width (1..5, 8, 16, 45), or kPack2 for p <= 32 (two rows per
 // wave instruction, lanes 0-31 and 32-63); 0 if p is too wide for the LDS
 // engine.  The value is the cone kernel's template argument and launch bucket.
 #ifndef RT_PACK_SMALL_ROWS
-#define RT_PACK_SMALL_ROWS 0
+#define RT_PACK_SMALL_ROWS 1
 #endif
 constexpr int kPack2 = 64;
 RT_HD inline int merge_slots(uint32_t p)
@@ -218,7 +224,8 @@ struct UnitDesc {
     // the blob's header counts (kHdrRuns .. kHdrRunOff), so the kernel issues
     // the unit's DMA after one scalar load instead of a dependent chain
     uint32_t nruns, entries, nb, slot_words, run_off;
-    uint32_t pad2[3];
+    uint32_t fill_chunks;  // 16-byte chunks of the bottom-level fill
+    uint32_t pad2[2];
 };
 static_assert(sizeof(UnitDesc) == 96, "UnitDesc layout");
 

@@ -214,6 +214,7 @@ struct UnitView {
     float stdnoise;
     uint32_t blob;            // word offset of the host-built blob (kNoBlob: none)
     int nruns, entries, nb, slot_words, run_off;   // its header counts
+    int fill_chunks;          // 16-byte chunks of the bottom-level fill
 };
 
 typedef const __attribute__((address_space(4))) uint32_t* const_u32_ptr;
@@ -252,6 +253,7 @@ __device__ __forceinline__ UnitView unit_view(const ConeArgs& a, int item, int t
     v.nb = uni((int)d.nb);
     v.slot_words = uni((int)d.slot_words);
     v.run_off = uni((int)d.run_off);
+    v.fill_chunks = uni((int)d.fill_chunks);
     return v;
 }
 
@@ -341,6 +343,7 @@ __device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t u, uin
     // transform blocks start 16-byte aligned and are padded to 4 floats
     const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(src, (((uint32_t)U.m * (uint32_t)p + 3u) & ~3u) * 4u);
     if (!C.table) {
+        ok = ok && SMAX != kPack2;    // short-row units always carry a blob
         C.al = (int)(((uint32_t)U.node_start * (uint32_t)p) & 3u);
         C.slots = false;
         C.nruns = C.entries = C.nb = 0;
@@ -362,8 +365,16 @@ __device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t u, uin
         C.nb = U.nb;
         C.slots = U.slot_words != 0;
         const int words = U.run_off;   // the LDS part: header .. slot tables
-        ok = ok && C.nb <= cap && C.entries <= kDescEntries && words <= kAuxWords &&
-             words >= kBlobHeader + C.entries + C.nb && C.nruns <= 64 * kConeWaves && (words & 3) == 0;
+        if constexpr (SMAX == kPack2) {
+            // at the end of the level buffer, above the fill and every level
+            // (validate_exec_plan; pack_blob_words)
+            C.aux = reinterpret_cast<uint32_t*>(buf + kLdsBufFloats) - words;
+            ok = ok && C.nb <= cap && 4 * U.fill_chunks + words <= kLdsBufFloats &&
+                 C.nb * p + words <= kLdsBufFloats && !C.slots;
+        } else {
+            ok = ok && C.nb <= cap && C.entries <= kDescEntries && words <= kAuxWords;
+        }
+        ok = ok && words >= kBlobHeader + C.entries + C.nb && C.nruns <= 64 * kConeWaves && (words & 3) == 0;
 #ifdef RT_STAMPS
         if (ts) ts[1] = __builtin_amdgcn_s_memtime() + (ok ? 0 : 0);
 #endif
@@ -376,7 +387,7 @@ __device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t u, uin
             if (lane < mine) sv = segs[wave + kConeWaves * lane];
             // the blob's LDS part: the last wave
             const __amdgpu_buffer_rsrc_t rb = buffer_rsrc(a.blob + U.blob, (uint32_t)words * 4u);
-            if (wave == kConeWaves - 1) dma_run(rb, 0u, words >> 2, (float*)aux, 0, 1, lane);
+            if (wave == kConeWaves - 1) dma_run(rb, 0u, words >> 2, (float*)const_cast<uint32_t*>(C.aux), 0, 1, lane);
             for (int i = 0; i < mine; ++i) {
                 const int c0 = __builtin_amdgcn_readlane((int)sv.x, i);
                 const int n = __builtin_amdgcn_readlane((int)sv.y, i);
@@ -622,49 +633,6 @@ __device__ __forceinline__ void merge_level2_dense(const UnitCtx& C, const float
     }
 }
 
-// kPack2 variant (p <= 32): register row i of a wave holds two output rows,
-// the wave's row 2i in lanes 0-31 and row 2i + 1 in lanes 32-63 (bin j =
-// lane & 31), so a wave instruction does the work of two rows instead of
-// leaving 32-48 of its 64 lanes idle.  Each half takes its row's offsets with
-// its own v_readlane and a select; otherwise as merge_level_dense (same
-// additions, same -0.0 carry masking).
-template <int RW, bool CARRIED>
-__device__ __forceinline__ void merge_level_packed(const UnitCtx& C, const float* src, int p, int l, int lane,
-                                                   int wave, int nr, float (&v)[RW][1], const int* loff)
-{
-    int ho = 0, to = 0, sh = 0, car = 0;
-    if (lane < nr) {
-        const uint32_t d = unit_desc(C, l, wave + kConeWaves * lane, p);
-        const uint32_t tc = (d >> 10) & 1023u;
-        sh = (int)(d >> 20);
-        ho = loff ? loff[d & 1023u] : (int)(d & 1023u) * p;
-        to = (tc == kCarried ? ho : (loff ? loff[tc] : (int)tc * p)) + sh;
-        car = tc == kCarried;
-    }
-    const bool hi = lane >= 32;
-    const int j = lane & 31;
-    const lds_cptr l1 = (lds_cptr)src + j;
-#pragma unroll
-    for (int i = 0; i < RW; ++i) {
-        const int hoi = hi ? __builtin_amdgcn_readlane(ho, 2 * i + 1) : __builtin_amdgcn_readlane(ho, 2 * i);
-        const int toi = hi ? __builtin_amdgcn_readlane(to, 2 * i + 1) : __builtin_amdgcn_readlane(to, 2 * i);
-        const int si = hi ? __builtin_amdgcn_readlane(sh, 2 * i + 1) : __builtin_amdgcn_readlane(sh, 2 * i);
-        uint32_t keep = 0xFFFFFFFFu, neg0 = 0u;
-        if (CARRIED) {
-            const int ci = hi ? __builtin_amdgcn_readlane(car, 2 * i + 1) : __builtin_amdgcn_readlane(car, 2 * i);
-            keep = ci ? 0u : 0xFFFFFFFFu;
-            neg0 = ~keep & 0x80000000u;
-        }
-        const lds_cptr hrow = l1 + hoi;
-        lds_cptr ta = l1 + toi;
-        lds_cptr tw = ta - p;
-        asm("" : "+v"(ta), "+v"(tw));
-        float x = lds_ld(j + si >= p ? tw : ta);
-        if (CARRIED) x = __uint_as_float((__float_as_uint(x) & keep) | neg0);
-        v[i][0] = __fadd_rn(hrow[0], x);
-    }
-}
-
 // Output level l == 0 of a non-final pass: straight from the staging
 // registers to global memory at byte offset st_o0 (the tile's rows are one
 // contiguous segment).
@@ -718,39 +686,6 @@ __device__ __forceinline__ void write_rows(float* base, float* dummy, const floa
                     if (64 * (k + 1) <= p || (k < S && lane + 64 * k < p)) orow[64 * k] = v[i][k];
                 }
             }
-        }
-    }
-}
-
-// kPack2 store / write-back: lane half h of register row i is the wave's row
-// 2i + h; halves past nr and bins past p store out of the buffer's range
-// (dropped) or to the LDS dummy word.
-template <int RW>
-__device__ __forceinline__ void store_rows_packed(const float (&v)[RW][1], int p, int lane, int wave, int nr,
-                                                  __amdgpu_buffer_rsrc_t rs, uint32_t st_o0)
-{
-    const int hi = lane >> 5, j = lane & 31;
-#pragma unroll
-    for (int i = 0; i < RW; ++i) {
-        if (2 * i < nr) {
-            const int k = 2 * i + hi;
-            const uint32_t o = (k < nr && j < p) ? st_o0 + (uint32_t)((wave + kConeWaves * k) * p + j) * 4u
-                                                 : 0x80000000u;
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][0]), rs, (int)o, 0, 0);
-        }
-    }
-}
-
-template <int RW>
-__device__ __forceinline__ void write_rows_packed(float* base, float* dummy, const float (&v)[RW][1], int p, int lane,
-                                                  int wave, int nr)
-{
-    const int hi = lane >> 5, j = lane & 31;
-#pragma unroll
-    for (int i = 0; i < RW; ++i) {
-        if (2 * i < nr) {
-            const int k = 2 * i + hi;
-            *((k < nr && j < p) ? base + (wave + kConeWaves * k) * p + j : dummy) = v[i][0];
         }
     }
 }
@@ -943,6 +878,116 @@ __device__ __forceinline__ void store_rows_slots(const float (&v)[RW][SMAX], int
     }
 }
 
+// kPack2 merge step (p <= 32; units always with a blob): register row i of
+// a wave holds two output rows, the wave's rows 2i (lanes 0-31) and 2i + 1
+// (lanes 32-63), bin j = lane & 31.  Every lane resolves its own row's
+// descriptor (the two halves read different table words; lanes of a half
+// read the same word) and computes its bin's wrapped indices itself: no
+// v_readlane and no per-row scalar work, so a wave instruction does the
+// work of two rows at the cost of one.  TWO: two levels per step, the
+// additions of merge_level2_dense; otherwise one level (carried size-1 nodes
+// add -0.0).  Rows past nrows and bins past p compute in-bounds garbage that
+// is never written back.
+template <int RW, bool TWO>
+__device__ __forceinline__ void merge_step_lanes(const UnitCtx& C, const float* src, int p, int lo, int lane, int wave,
+                                                 int nrows, float (&v)[RW][1], const int* loff)
+{
+    // an opaque copy of the lane, so per-row addresses are not hoisted out of
+    // the level loop into 2 x RW long-lived registers (spills)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int h = ln >> 5, j = ln & 31;
+    const uint32_t* const desc = desc_table(C);
+    const int dl = desc_offset(C, lo);
+    const int dn = TWO ? desc_offset(C, lo + 1) : 0;
+    const lds_cptr sp = (lds_cptr)src;
+    // groups of G register rows without a branch between them, so the
+    // descriptor chains (2-4 dependent LDS reads per row) of a group overlap
+    constexpr int G = 4;
+    auto row = [&](int i) {
+        int r = wave + kConeWaves * (2 * i + h);
+        r = r < nrows ? r : nrows - 1;
+        if constexpr (TWO) {
+            const uint32_t d0 = desc[dl + r];
+            const uint32_t dh = desc[dn + (int)(d0 & 1023u)];
+            const uint32_t dt = desc[dn + (int)((d0 >> 10) & 1023u)];
+            const int sh = (int)(d0 >> 20), sH = (int)(dh >> 20), sT = (int)(dt >> 20);
+            const uint32_t q0 = dh & 1023u, q1 = (dh >> 10) & 1023u, q2 = dt & 1023u, q3 = (dt >> 10) & 1023u;
+            const int o0 = loff ? loff[q0] : (int)q0 * p;
+            const int o1 = loff ? loff[q1] : (int)q1 * p;
+            const int o2 = loff ? loff[q2] : (int)q2 * p;
+            const int o3 = loff ? loff[q3] : (int)q3 * p;
+            int i1 = j + sH, i2 = j + sh, i3 = j + sh + sT;
+            i1 = i1 >= p ? i1 - p : i1;
+            i2 = i2 >= p ? i2 - p : i2;
+            i3 = i3 >= p ? i3 - p : i3;
+            i3 = i3 >= p ? i3 - p : i3;
+            const float x0 = lds_ld(sp + o0 + j);
+            const float x1 = lds_ld(sp + o1 + i1);
+            const float x2 = lds_ld(sp + o2 + i2);
+            const float x3 = lds_ld(sp + o3 + i3);
+            v[i][0] = __fadd_rn(__fadd_rn(x0, x1), __fadd_rn(x2, x3));
+        } else {
+            const uint32_t d = desc[dl + r];
+            const uint32_t tc = (d >> 10) & 1023u;
+            const bool car = tc == kCarried;
+            const int sh = (int)(d >> 20);
+            const int ho = loff ? loff[d & 1023u] : (int)(d & 1023u) * p;
+            const int to = car ? ho : (loff ? loff[tc] : (int)tc * p);
+            int i1 = j + sh;
+            i1 = i1 >= p ? i1 - p : i1;
+            const float x0 = lds_ld(sp + ho + j);
+            float x1 = lds_ld(sp + to + i1);
+            x1 = car ? -0.0f : x1;
+            v[i][0] = __fadd_rn(x0, x1);
+        }
+    };
+#pragma unroll
+    for (int g = 0; g < RW; g += G) {
+        if (wave + kConeWaves * 2 * g < nrows) {
+#pragma unroll
+            for (int i = g; i < (g + G < RW ? g + G : RW); ++i) row(i);
+        }
+    }
+}
+
+template <int RW>
+__device__ __forceinline__ void write_rows_lanes(float* base, float* dummy, const float (&v)[RW][1], int p, int lane,
+                                                 int wave, int nrows)
+{
+    // an opaque copy of the lane, so per-row addresses are not hoisted out of
+    // the level loop into 2 x RW long-lived registers (spills)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int h = ln >> 5, j = ln & 31;
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+        if (wave + kConeWaves * 2 * i < nrows) {
+            const int r = wave + kConeWaves * (2 * i + h);
+            *((r < nrows && j < p) ? base + r * p + j : dummy) = v[i][0];
+        }
+    }
+}
+
+template <int RW>
+__device__ __forceinline__ void store_rows_lanes(const float (&v)[RW][1], int p, int lane, int wave, int nrows,
+                                                 __amdgpu_buffer_rsrc_t rs, uint32_t st_o0)
+{
+    // an opaque copy of the lane, so per-row addresses are not hoisted out of
+    // the level loop into 2 x RW long-lived registers (spills)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int h = ln >> 5, j = ln & 31;
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+        if (wave + kConeWaves * 2 * i < nrows) {
+            const int r = wave + kConeWaves * (2 * i + h);
+            const uint32_t o = (r < nrows && j < p) ? st_o0 + (uint32_t)(r * p + j) * 4u : 0x80000000u;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][0]), rs, (int)o, 0, 0);
+        }
+    }
+}
+
 // All merge levels of one unit, deepest first, in place in the dense rows
 // at `base`.  SMAX >= ceil(p/64) slots per row, RW rows per wave
 // (lds_row_capacity(p, SMAX) guarantees ceil(rows/8) <= RW at every level).
@@ -965,7 +1010,29 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
     // deepest first; two levels per step (merge_level2_dense) once no level
     // below the step's output holds size-1 nodes, single steps before that
     // and for a last odd level
-    const bool fuse = (flags & kConeFuse2) && SMAX != kPack2;
+    const bool fuse = (flags & kConeFuse2) != 0;
+    if constexpr (SMAX == kPack2) {
+        for (int l = L - 1; l >= 0;) {
+            const bool two = fuse && l >= 1 && (tile || (node_size >> l) >= 2);
+            const int lo = two ? l - 1 : l;
+            const int nrows = rows_at(C, lo);
+            float v[RW][1];
+            const bool first = l == L - 1;
+            const float* src = first ? src0 : base;
+            const int* lo_src = first ? loff : nullptr;
+            if (two) merge_step_lanes<RW, true>(C, src, p, lo, lane, wave, nrows, v, lo_src);
+            else merge_step_lanes<RW, false>(C, src, p, lo, lane, wave, nrows, v, lo_src);
+            l = lo - 1;
+            if (lo == 0 && st) {
+                store_rows_lanes<RW>(v, p, lane, wave, nrows, rs, st_o0);
+                return;
+            }
+            if (!(flags & kConeDiagNoBarrier)) lds_barrier();
+            if (!(flags & kConeDiagNoWrite)) write_rows_lanes<RW>(base, dummy, v, p, lane, wave, nrows);
+            if (!(flags & kConeDiagNoBarrier)) lds_barrier();
+        }
+        return;
+    }
     if constexpr (SMAX <= 5) {
         if (C.slots && fuse) {
             // row-slot steps (the host's slot tables follow this step order)
@@ -1004,29 +1071,20 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
         const bool first = l == L - 1;
         const float* src = first ? src0 : base;
         const int* lo_src = first ? loff : nullptr;
-        if constexpr (SMAX == kPack2) {
-            if (carried)
-                merge_level_packed<RW, true>(C, src, p, l, lane, wave, nr, v, lo_src);
-            else
-                merge_level_packed<RW, false>(C, src, p, l, lane, wave, nr, v, lo_src);
-        } else {
-            if (two)
-                merge_level2_dense<S, RW>(C, src, p, lo, lane, wave, nr, v, lo_src);
-            else if (carried)
-                merge_level_dense<S, RW, true>(C, src, p, l, lane, wave, nr, v, lo_src);
-            else
-                merge_level_dense<S, RW, false>(C, src, p, l, lane, wave, nr, v, lo_src);
-        }
+        if (two)
+            merge_level2_dense<S, RW>(C, src, p, lo, lane, wave, nr, v, lo_src);
+        else if (carried)
+            merge_level_dense<S, RW, true>(C, src, p, l, lane, wave, nr, v, lo_src);
+        else
+            merge_level_dense<S, RW, false>(C, src, p, l, lane, wave, nr, v, lo_src);
         l = lo - 1;
         if (lo == 0 && st) {
-            if constexpr (SMAX == kPack2) store_rows_packed<RW>(v, p, lane, wave, nr, rs, st_o0);
-            else store_rows<S, RW>(v, p, lane, wave, nr, rs, st_o0);
+            store_rows<S, RW>(v, p, lane, wave, nr, rs, st_o0);
             return;
         }
         if (!(flags & kConeDiagNoBarrier)) lds_barrier();
         if (!(flags & kConeDiagNoWrite)) {
-            if constexpr (SMAX == kPack2) write_rows_packed<RW>(base, dummy, v, p, lane, wave, nr);
-            else write_rows<S, RW>(base, dummy, v, p, lane, wave, nr);
+            write_rows<S, RW>(base, dummy, v, p, lane, wave, nr);
         }
         if (!(flags & kConeDiagNoBarrier)) lds_barrier();
     }

@@ -164,9 +164,11 @@ ConeNeed cone_need(uint32_t node_size, uint32_t s0, uint32_t s1, int levels, uin
 
 static bool fits(const ConeNeed& n, uint32_t p, int smax)
 {
-    return !n.degenerate && n.max_rows <= lds_row_capacity(p, smax) && n.max_floats <= kLdsDataFloats &&
-           n.ranges <= kMaxRanges && 4 * fill_chunks_bound(n.rows_bottom, (int)p, n.runs_bottom) <= kLdsBufFloats &&
-           n.entries <= kDescEntries;
+    if (n.degenerate || n.max_rows > lds_row_capacity(p, smax) || n.ranges > kMaxRanges) return false;
+    const int fill = 4 * fill_chunks_bound(n.rows_bottom, (int)p, n.runs_bottom);
+    if (smax == kPack2)   // the blob at the end of the level buffer (pack_blob_words)
+        return std::max(fill, n.max_floats) + pack_blob_words(n.entries, n.rows_bottom) <= kLdsBufFloats;
+    return n.max_floats <= kLdsDataFloats && fill <= kLdsBufFloats && n.entries <= kDescEntries;
 }
 
 // Per-transform schedule: list of passes, each a list of (node, tile, levels).
@@ -398,17 +400,22 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
     // host-built metadata of the tile items (trial-independent, shared by a
     // launch's whole batch)
     std::vector<int> slot_rw(out.items.size(), 0);
+    std::vector<bool> packed(out.items.size(), false);
     for (const Launch& L : out.launches) {
         // row-slot tables for the kernel instances that use them (SMAX <= 5)
         const int rw = L.smax <= 5 ? (L.rw ? (int)L.rw : merge_rows_per_wave((int)L.smax)) : 0;
-        for (uint32_t i = L.first; i < L.first + L.count; ++i) slot_rw[i] = rw;
+        for (uint32_t i = L.first; i < L.first + L.count; ++i) {
+            slot_rw[i] = rw;
+            packed[i] = L.smax == (uint32_t)kPack2;
+        }
     }
     for (size_t i = 0; i < out.items.size(); ++i) {
         ConeItem& it = out.items[i];
         it.pad = kNoBlob;
         // whole units: a descriptor table only when it fits the LDS area
-        // (otherwise the kernel derives the node partition on the fly)
-        if (it.mode != kModeTile &&
+        // (otherwise the kernel derives the node partition on the fly);
+        // kPack2 units always have one (in their level buffer)
+        if (!packed[i] && it.mode != kModeTile &&
             ((uint64_t)it.levels * it.node_size > (uint64_t)kDescEntries || it.node_size > (uint32_t)kMaxRows))
             continue;
         it.pad = (uint32_t)out.blob.size();
@@ -612,10 +619,69 @@ void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, std::vector<ui
     w[kHdrBottom] = nb;
     w[kHdrSlotWords] = (uint32_t)slot_area.size();
     w[kHdrRunOff] = (uint32_t)runoff;
+    w[kHdrFill] = cb;
     std::copy(desc_v.begin(), desc_v.end(), w + kBlobHeader);
     std::copy(loff_v.begin(), loff_v.end(), w + kBlobHeader + entries);
     std::copy(slot_area.begin(), slot_area.end(), w + kBlobHeader + entries + nb);
     std::copy(segs.begin(), segs.end(), w + runoff);
+}
+
+// A unit's blob as the kernel will read it: the DMA segments tile the fill
+// [0, fill chunks) in order, each <= 64 chunks inside the level buffer; every
+// row-slot table covers its step's output rows exactly once, a pair's rows
+// sharing head and tail rows with consecutive shifts (never carried rows),
+// within the register rows of the launch's kernel instance.
+static void validate_blob(const ConeItem& it, uint32_t p, int smax, int rw, const uint32_t* w)
+{
+    const uint32_t L = it.levels;
+    const uint32_t nseg = w[kHdrRuns], entries = w[kHdrEntries], nb = w[kHdrBottom];
+    const uint32_t slot_words = w[kHdrSlotWords], runoff = w[kHdrRunOff], fill = w[kHdrFill];
+    if (runoff < (uint32_t)kBlobHeader + entries + nb + slot_words || (runoff & 3u) || nb != w[kHdrRows + L])
+        throw std::runtime_error("schedule: malformed unit blob header");
+    if (4 * fill > (uint32_t)kLdsBufFloats) throw std::runtime_error("schedule: unit fill exceeds the LDS level buffer");
+    uint32_t c = 0;
+    for (uint32_t i = 0; i < nseg; ++i) {
+        const uint32_t* g = w + runoff + 4 * i;
+        if (g[0] != c || g[1] == 0 || g[1] > 64) throw std::runtime_error("schedule: DMA segments do not tile the fill");
+        c += g[1];
+    }
+    if (c != fill) throw std::runtime_error("schedule: DMA segments do not tile the fill");
+    const uint32_t* desc = w + kBlobHeader;
+    for (uint32_t l = 0; l < L; ++l)
+        if (w[kHdrDesc + l] + w[kHdrRows + l] > entries) throw std::runtime_error("schedule: descriptor table overrun");
+    if (!slot_words) {
+        if (smax <= 5 && L > 0) throw std::runtime_error("schedule: unit without row-slot tables");
+        return;
+    }
+    const bool tile = it.mode == kModeTile;
+    const int Q = (rw + 1) / 2;
+    for (int l = (int)L - 1; l >= 0;) {
+        const bool two = l >= 1 && (tile || (it.node_size >> l) >= 2);
+        const int lo = two ? l - 1 : l;
+        const uint32_t n = w[kHdrRows + lo], so = w[kHdrSlotOff + lo];
+        if (so < (uint32_t)kBlobHeader + entries + nb || so >= runoff) throw std::runtime_error("schedule: row-slot table outside the blob");
+        const uint32_t ns = w[so];
+        if (ns > (uint32_t)(kConeWaves * Q) || so + 1 + ns > runoff) throw std::runtime_error("schedule: row-slot table overrun");
+        std::vector<uint8_t> seen(n, 0);
+        const uint32_t* d = desc + w[kHdrDesc + lo];
+        for (uint32_t g = 0; g < ns; ++g) {
+            const uint32_t sw = w[so + 1 + g], ra = sw & 1023u, rb = (sw >> 10) & 1023u, kind = sw >> 20;
+            const int q = (int)g / kConeWaves;
+            const bool two_rows = kind == kSlotTwo || kind == kSlotPair;
+            if (kind > kSlotPair || ra >= n || (two_rows && (rb >= n || 2 * q + 1 >= rw)))
+                throw std::runtime_error("schedule: bad row slot");
+            if (seen[ra]++ || (two_rows && seen[rb]++)) throw std::runtime_error("schedule: row slot covers a row twice");
+            if (kind == kSlotPair) {
+                const uint32_t a = d[ra], b = d[rb];
+                if (rb != ra + 1 || ((a ^ b) & 0xFFFFFu) || ((a >> 10) & 1023u) == kCarriedRow ||
+                    (b >> 20) != ((a >> 20) + 1) % p)
+                    throw std::runtime_error("schedule: row pair without shared head/tail rows");
+            }
+        }
+        for (uint32_t r = 0; r < n; ++r)
+            if (!seen[r]) throw std::runtime_error("schedule: row-slot table misses a row");
+        l = lo - 1;
+    }
 }
 
 void validate_exec_plan(const ExecPlan& ex, bool snr_epilogue)
@@ -654,10 +720,22 @@ void validate_exec_plan(const ExecPlan& ex, bool snr_epilogue)
             const int bottom = it.mode == kModeTile ? need.rows_bottom : (int)it.node_size;
             if (4 * fill_chunks_bound(bottom, (int)X.p, it.mode == kModeTile ? 1 << it.levels : 1) > kLdsBufFloats)
                 throw std::runtime_error("schedule: unit fill exceeds the LDS level buffer");
-            if (it.mode == kModeTile && (need.entries > kDescEntries || it.pad == kNoBlob))
+            if (L.smax == (uint32_t)kPack2) {
+                // blob at the end of the level buffer, clear of the fill and every level
+                if (it.pad == kNoBlob) throw std::runtime_error("schedule: short-row unit without a descriptor table");
+                const uint32_t* h = ex.blob.data() + it.pad;
+                const int top = std::max<int>(4 * (int)h[kHdrFill], rows * (int)X.p);
+                if (top + (int)h[kHdrRunOff] > kLdsBufFloats)
+                    throw std::runtime_error("schedule: short-row unit and its descriptor table exceed the level buffer");
+            } else if (it.mode == kModeTile && (need.entries > kDescEntries || it.pad == kNoBlob)) {
                 throw std::runtime_error("schedule: tile descriptor table exceeds its LDS area");
+            }
             // the launch's kernel instance stages enough register rows for every level
             const int rw = L.rw ? (int)L.rw : merge_rows_per_wave((int)L.smax);
+            if (it.pad != kNoBlob) {
+                if ((size_t)it.pad + kBlobHeader > ex.blob.size()) throw std::runtime_error("schedule: blob outside the plan");
+                validate_blob(it, X.p, (int)L.smax, rw, ex.blob.data() + it.pad);
+            }
             if (rows > kConeWaves * rw * row_pack((int)L.smax) || rows > lds_row_capacity(X.p, (int)L.smax))
                 throw std::runtime_error("schedule: unit rows exceed its kernel instance's register rows");
             if (L.pass == last_pass[it.xform]) {

@@ -204,3 +204,20 @@ def test_periodogram_object():
     assert pg.tobs == 10.0
     assert Periodogram.from_dict(pg.to_dict()).metadata == pg.metadata
     assert Metadata({})["dm"] is None
+
+
+def test_ffa_schedules_validate(lib):
+    """The pass schedule rt_ffa2 runs for every golden FFA shape, plus edge
+    shapes (one row, short / long rows, node sizes around the LDS capacity),
+    passes the host validation the kernel relies on (unit blobs: DMA
+    segments tile the fill, row-slot tables cover every row once, row pairs
+    share head and tail rows)."""
+    from tests.golden import inputs
+    shapes = {(m, p) for m, p, _ in inputs.FFA_CASES}
+    shapes |= {(1, 1), (1, 260), (2, 1), (3, 17), (64, 32), (65, 33), (384, 16), (385, 16), (1000, 31),
+               (72, 250), (73, 250), (5000, 257), (4097, 64), (300, 700), (40, 2880)}
+    n = ctypes.c_uint64()
+    for m, p in sorted(shapes):
+        assert lib.rt_ffa_schedule_check(m, p, ctypes.byref(n)) == 0, (m, p, lib.rt_last_error())
+        assert n.value >= 1
+    assert lib.rt_ffa_schedule_check(0, 16, None) == 1

@@ -29,8 +29,13 @@ def main():
     from riptide_amd import _lib, engine
     L = _lib.load()
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-    n = 1 << 23
-    plan = engine.PeriodogramPlan.for_search(n, 256e-6, 0.1, 10.0, 240, 260, ducy_max=0.05)
+    cfg = sys.argv[2] if len(sys.argv) > 2 else "cfg2"
+    if cfg == "cfg4":
+        n = 1 << 22
+        plan = engine.PeriodogramPlan.for_search(n, 64e-6, 0.002, 0.5, 16, 32, ducy_max=0.2)
+    else:
+        n = 1 << 23
+        plan = engine.PeriodogramPlan.for_search(n, 256e-6, 0.1, 10.0, 240, 260, ducy_max=0.05)
     buf = (ctypes.c_uint64 * 8)()
     _lib.check(L.rt_diag_stamps(buf, 1))     # allocates the device records
     x = torch.randn((B, n), device="cuda", dtype=torch.float32)

@@ -13,11 +13,11 @@ int main(int argc, char** argv)
 {
     PgramParams a;
     a.size = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : (1u << 23);
-    a.tsamp = 256e-6;
-    a.pmin = 0.1;
-    a.pmax = 10.0;
-    a.bmin = 240;
-    a.bmax = 260;
+    a.tsamp = argc > 2 ? std::atof(argv[2]) : 256e-6;
+    a.pmin = argc > 3 ? std::atof(argv[3]) : 0.1;
+    a.pmax = argc > 4 ? std::atof(argv[4]) : 10.0;
+    a.bmin = argc > 5 ? std::atoi(argv[5]) : 240;
+    a.bmax = argc > 6 ? std::atoi(argv[6]) : 260;
     PgramPlan pg;
     build_pgram_plan(a, pg);
     std::vector<FfaXform> xf;
@@ -32,7 +32,7 @@ int main(int argc, char** argv)
     }
     ExecPlan ex;
     build_exec_plan(xf, true, 6, 1ull << 40, ex);
-    double rows_tot = 0, items_tot = 0;
+    double rows_tot = 0, items_tot = 0, noblob = 0, noblob_rows = 0, blob_units = 0;
     double issued = 0, useful = 0, ideal = 0, steps = 0, units = 0;
     std::map<int, double> by_rw_issued, by_rw_useful;
     for (const Launch& L : ex.launches) {
@@ -48,6 +48,7 @@ int main(int argc, char** argv)
                 return (int)it.node_size;
             };
             units += 1;
+            if (it.pad == kNoBlob) { noblob += 1; noblob_rows += it.node_size; } else blob_units += 1;
             if (it.pad != kNoBlob) {
                 const uint32_t* w = ex.blob.data() + it.pad;
                 const uint32_t* desc = w + kBlobHeader + 4 * w[24];
@@ -95,6 +96,7 @@ int main(int argc, char** argv)
                 units, steps, issued, useful, ideal, useful / issued);
     std::printf("LDS time at 2 clk/read over 256 CUs @2.4GHz: issued %.3f ms, useful %.3f ms\n",
                 issued * 2 / 256 / 2.4e9 * 1e3, useful * 2 / 256 / 2.4e9 * 1e3);
+    std::printf("units without blob %.0f (avg rows %.1f), with blob %.0f\n", noblob, noblob_rows / (noblob > 0 ? noblob : 1), blob_units);
     std::printf("table units: reads by rows %.3e, by row pairs %.3e (%.3f)\n", rows_tot, items_tot, items_tot / rows_tot);
     for (auto& kv : by_rw_issued)
         std::printf("  rw %2d issued %.3e useful %.3e (%.3f)\n", kv.first, kv.second, by_rw_useful[kv.first],
