@@ -95,7 +95,7 @@ RT_HD inline int fill_chunks_bound(int n, int p, int runs) { return (n * p + 6 *
 // offsets; no slot tables) at the end of their own level buffer instead of
 // the fixed metadata area, so the descriptor table may hold every level of
 // a 384-row unit.
-RT_HD inline int pack_blob_words(int entries, int nb) { return (kBlobHeader + entries + nb + 3) & ~3; }
+RT_HD inline int pack_blob_words(int entries, int nb) { return (kBlobHeader + entries + nb + 2 * kMaxLevels + 4) & ~3; }
 
 // Merge variant for rows of p phase bins: slots per row rounded up to an
 // instantiated width (1..5, 8, 16, 45), or kPack2 for p <= 32 (two rows per

@@ -369,8 +369,7 @@ __device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t u, uin
             // at the end of the level buffer, above the fill and every level
             // (validate_exec_plan; pack_blob_words)
             C.aux = reinterpret_cast<uint32_t*>(buf + kLdsBufFloats) - words;
-            ok = ok && C.nb <= cap && 4 * U.fill_chunks + words <= kLdsBufFloats &&
-                 C.nb * p + words <= kLdsBufFloats && !C.slots;
+            ok = ok && C.nb <= cap && 4 * U.fill_chunks + words <= kLdsBufFloats && C.nb * p + words <= kLdsBufFloats;
         } else {
             ok = ok && C.nb <= cap && C.entries <= kDescEntries && words <= kAuxWords;
         }
@@ -898,8 +897,8 @@ __device__ __forceinline__ void merge_step_lanes(const UnitCtx& C, const float* 
     asm volatile("" : "+v"(ln));
     const int h = ln >> 5, j = ln & 31;
     const uint32_t* const desc = desc_table(C);
-    const int dl = desc_offset(C, lo);
-    const int dn = TWO ? desc_offset(C, lo + 1) : 0;
+    const int dl = TWO ? 0 : desc_offset(C, lo);
+    const uint2* const step = reinterpret_cast<const uint2*>(TWO ? slot_table(C, lo) : C.aux);
     const lds_cptr sp = (lds_cptr)src;
     // groups of G register rows without a branch between them, so the
     // descriptor chains (2-4 dependent LDS reads per row) of a group overlap
@@ -908,19 +907,17 @@ __device__ __forceinline__ void merge_step_lanes(const UnitCtx& C, const float* 
         int r = wave + kConeWaves * (2 * i + h);
         r = r < nrows ? r : nrows - 1;
         if constexpr (TWO) {
-            const uint32_t d0 = desc[dl + r];
-            const uint32_t dh = desc[dn + (int)(d0 & 1023u)];
-            const uint32_t dt = desc[dn + (int)((d0 >> 10) & 1023u)];
-            const int sh = (int)(d0 >> 20), sH = (int)(dh >> 20), sT = (int)(dt >> 20);
-            const uint32_t q0 = dh & 1023u, q1 = (dh >> 10) & 1023u, q2 = dt & 1023u, q3 = (dt >> 10) & 1023u;
+            // the host-resolved row: source rows q0..q3 of level lo + 2, rolls
+            const uint2 e = step[r];
+            const uint32_t q0 = e.x & 1023u, q1 = (e.x >> 10) & 1023u, q2 = (e.x >> 20) & 1023u, q3 = e.y & 1023u;
+            const int sH = (int)((e.y >> 10) & 63u), sh = (int)((e.y >> 16) & 63u), sTT = (int)((e.y >> 22) & 63u);
             const int o0 = loff ? loff[q0] : (int)q0 * p;
             const int o1 = loff ? loff[q1] : (int)q1 * p;
             const int o2 = loff ? loff[q2] : (int)q2 * p;
             const int o3 = loff ? loff[q3] : (int)q3 * p;
-            int i1 = j + sH, i2 = j + sh, i3 = j + sh + sT;
+            int i1 = j + sH, i2 = j + sh, i3 = j + sTT;
             i1 = i1 >= p ? i1 - p : i1;
             i2 = i2 >= p ? i2 - p : i2;
-            i3 = i3 >= p ? i3 - p : i3;
             i3 = i3 >= p ? i3 - p : i3;
             const float x0 = lds_ld(sp + o0 + j);
             const float x1 = lds_ld(sp + o1 + i1);

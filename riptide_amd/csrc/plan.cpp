@@ -419,7 +419,7 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
             ((uint64_t)it.levels * it.node_size > (uint64_t)kDescEntries || it.node_size > (uint32_t)kMaxRows))
             continue;
         it.pad = (uint32_t)out.blob.size();
-        build_tile_blob(it, out.xf[it.xform].p, slot_rw[i], out.blob);
+        build_tile_blob(it, out.xf[it.xform].p, slot_rw[i], packed[i], out.blob);
     }
     validate_exec_plan(out, snr_epilogue);
 }
@@ -480,7 +480,7 @@ static void build_row_slots(const uint32_t* d, uint32_t n, uint32_t p, int rw, s
     }
 }
 
-void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, std::vector<uint32_t>& out)
+void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, bool packed, std::vector<uint32_t>& out)
 {
     struct R { uint32_t size, lo, hi; uint32_t start; uint32_t base; };
     const int L = it.levels;
@@ -570,7 +570,50 @@ void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, std::vector<ui
     // step where no level below the output holds size-1 nodes)
     std::vector<uint32_t> slot_area;
     uint32_t slot_off[kMaxLevels + 1] = {};
-    if (slot_rw > 0) {
+    if (packed) {
+        // kPack2: every lane resolves its own row, so a two-level step gets
+        // its rows pre-resolved (one 8-byte read per row instead of three
+        // dependent descriptor reads): the four source rows of level lo + 2
+        // and the three rolls (sH, sh, (sh + sT) mod p), and only the levels
+        // single steps read keep their descriptors
+        std::vector<bool> keep(L + 1, false), fused(L + 1, false);
+        std::vector<uint32_t> rel(L + 1, 0);
+        for (int l = L - 1; l >= 0;) {
+            const bool two = l >= 1 && (tile || (it.node_size >> l) >= 2);
+            const int lo = two ? l - 1 : l;
+            if (!two) {
+                keep[lo] = true;
+            } else {
+                fused[lo] = true;
+                rel[lo] = (uint32_t)slot_area.size();   // even: two words per row
+                for (uint32_t r = 0; r < nrows[lo]; ++r) {
+                    const uint32_t d0 = desc[doff[lo] + r];
+                    const uint32_t dh = desc[doff[lo + 1] + (d0 & 1023u)];
+                    const uint32_t dt = desc[doff[lo + 1] + ((d0 >> 10) & 1023u)];
+                    const uint32_t sh = d0 >> 20, sH = dh >> 20, sTT = ((d0 >> 20) + (dt >> 20)) % p;
+                    slot_area.push_back((dh & 1023u) | (((dh >> 10) & 1023u) << 10) | ((dt & 1023u) << 20));
+                    slot_area.push_back(((dt >> 10) & 1023u) | (sH << 10) | (sh << 16) | (sTT << 22));
+                }
+            }
+            l = lo - 1;
+        }
+        // compact descriptor table: the kept levels only
+        std::vector<uint32_t> dc;
+        for (int l = 0; l < L; ++l) {
+            const uint32_t o0 = doff[l];
+            doff[l] = (uint32_t)dc.size();
+            if (keep[l]) dc.insert(dc.end(), desc_v.begin() + o0, desc_v.begin() + o0 + nrows[l]);
+        }
+        desc_v.swap(dc);
+        desc = desc_v.data();
+        entries = (uint32_t)desc_v.size();
+        // the step tables start 8-byte aligned (uint2 reads)
+        const uint32_t base0 = kBlobHeader + entries + nb;
+        if (base0 & 1u) slot_area.insert(slot_area.begin(), 0u);
+        const uint32_t base = base0 + (base0 & 1u);
+        for (int l = 0; l <= L; ++l)
+            if (fused[l]) slot_off[l] = base + rel[l];
+    } else if (slot_rw > 0) {
         std::vector<uint32_t> sl;
         for (int l = L - 1; l >= 0;) {
             const bool two = l >= 1 && (tile || (it.node_size >> l) >= 2);
@@ -647,13 +690,36 @@ static void validate_blob(const ConeItem& it, uint32_t p, int smax, int rw, cons
     }
     if (c != fill) throw std::runtime_error("schedule: DMA segments do not tile the fill");
     const uint32_t* desc = w + kBlobHeader;
-    for (uint32_t l = 0; l < L; ++l)
-        if (w[kHdrDesc + l] + w[kHdrRows + l] > entries) throw std::runtime_error("schedule: descriptor table overrun");
+    if (smax != kPack2)
+        for (uint32_t l = 0; l < L; ++l)
+            if (w[kHdrDesc + l] + w[kHdrRows + l] > entries) throw std::runtime_error("schedule: descriptor table overrun");
+    const bool tile = it.mode == kModeTile;
+    if (smax == kPack2) {
+        // pre-resolved two-level steps: source rows inside level lo + 2, rolls < p
+        for (int l = (int)L - 1; l >= 0;) {
+            const bool two = l >= 1 && (tile || (it.node_size >> l) >= 2);
+            const int lo = two ? l - 1 : l;
+            if (two) {
+                const uint32_t so = w[kHdrSlotOff + lo], n = w[kHdrRows + lo], nsrc = w[kHdrRows + lo + 2];
+                if (!so || (so & 1u) || so + 2 * n > runoff) throw std::runtime_error("schedule: step table outside the blob");
+                for (uint32_t r = 0; r < n; ++r) {
+                    const uint32_t a = w[so + 2 * r], b = w[so + 2 * r + 1];
+                    const uint32_t s1 = (b >> 10) & 63u, s2 = (b >> 16) & 63u, s3 = (b >> 22) & 63u;
+                    if ((a & 1023u) >= nsrc || ((a >> 10) & 1023u) >= nsrc || ((a >> 20) & 1023u) >= nsrc ||
+                        (b & 1023u) >= nsrc || s1 >= p || s2 >= p || s3 >= p)
+                        throw std::runtime_error("schedule: bad step table entry");
+                }
+            } else if (w[kHdrDesc + lo] + w[kHdrRows + lo] > entries) {
+                throw std::runtime_error("schedule: descriptor table overrun");
+            }
+            l = lo - 1;
+        }
+        return;
+    }
     if (!slot_words) {
         if (smax <= 5 && L > 0) throw std::runtime_error("schedule: unit without row-slot tables");
         return;
     }
-    const bool tile = it.mode == kModeTile;
     const int Q = (rw + 1) / 2;
     for (int l = (int)L - 1; l >= 0;) {
         const bool two = l >= 1 && (tile || (it.node_size >> l) >= 2);

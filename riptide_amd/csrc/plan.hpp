@@ -83,7 +83,11 @@ struct ExecPlan {
 //   [segments offset, + 4 segments)  per segment (one LDS-DMA wave
 //             instruction): first LDS chunk, chunks (<= 64), first source
 //             chunk (16 bytes) in the transform block, 0
-void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, std::vector<uint32_t>& out);
+// packed (kPack2 units): instead of row-slot tables, every two-level step
+// gets a table of its output rows pre-resolved (2 words per row: the four
+// source rows, the three rolls) and the descriptor table keeps only the
+// levels single steps read.
+void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, bool packed, std::vector<uint32_t>& out);
 
 // Schedule a list of transforms (p, m, rows_eval, src_off, snr_row, stdnoise
 // filled in by the caller).  With snr_epilogue the last pass of every
