@@ -471,6 +471,17 @@ typedef const __attribute__((address_space(3))) float* lds_cptr;
 #ifndef RT_MERGE_PIPE
 #define RT_MERGE_PIPE 0
 #endif
+#ifndef RT_SLOT_OPAQUE_LANE
+#define RT_SLOT_OPAQUE_LANE 0
+#endif
+// A/B knobs of the row-slot merge (measured, ms per cfg2 trial): a template
+// constant instead of the run-time loff test in the slot resolution 8.96 vs
+// 8.81 (the second instance of the slot loop costs more than the branches it
+// removes; kept off -- the short-row path, whose branches sat in its row
+// loop, gained: cfg4 1.64 -> 1.40); an opaque lane copy per step 9.04.
+#ifndef RT_SLOT_FIRST
+#define RT_SLOT_FIRST 0
+#endif
 
 __device__ __forceinline__ float lds_ld(lds_cptr p) { return *(const volatile __attribute__((address_space(3))) float*)p; }
 
@@ -754,13 +765,16 @@ __device__ __forceinline__ void row_terms(lds_cptr l1, int p, int lane, int i, i
     }
 }
 
-template <int SMAX, int RW, bool TWO>
+template <int SMAX, int RW, bool TWO, bool FIRST>
 __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* src, int p, int lo, int lane,
                                                  int wave, float (&v)[RW][SMAX], const int* loff, uint32_t& sw,
                                                  int& nq)
 {
     constexpr int Q = (RW + 1) / 2;
     static_assert(Q <= 32, "row slots: one lane per slot row");
+#if RT_SLOT_OPAQUE_LANE
+    asm volatile("" : "+v"(lane));
+#endif
     const uint32_t* st = slot_table(C, lo);
     const int ns = uni((int)st[0]);
     nq = uni(ns > wave ? (ns - wave + kConeWaves - 1) / kConeWaves : 0);
@@ -770,6 +784,9 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
     const bool act = qi < nq && (lane < 32 || (sw >> 20) == kSlotTwo);
     const int r = lane < 32 ? (int)(sw & 1023u) : (int)((sw >> 10) & 1023u);
     const uint32_t* const desc = desc_table(C);
+    // the first step reads the bottom level through its row offsets: a
+    // template constant (a run-time test of loff made every offset a branch)
+    const bool use_loff = RT_SLOT_FIRST ? FIRST : loff != nullptr;
     int o0 = 0, o1 = 0, o2 = 0, o3 = 0, s1 = 0, s2 = 0, s3 = 0;
     if (act) {
         if constexpr (TWO) {
@@ -780,10 +797,10 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
             int sTT = sh + sT;
             sTT = sTT >= p ? sTT - p : sTT;
             const uint32_t r0 = dh & 1023u, r1 = (dh >> 10) & 1023u, r2 = dt & 1023u, r3 = (dt >> 10) & 1023u;
-            o0 = (loff ? loff[r0] : (int)r0 * p);
-            o1 = (loff ? loff[r1] : (int)r1 * p) + sH;
-            o2 = (loff ? loff[r2] : (int)r2 * p) + sh;
-            o3 = (loff ? loff[r3] : (int)r3 * p) + sTT;
+            o0 = (use_loff ? loff[r0] : (int)__umul24(r0, (uint32_t)p));
+            o1 = (use_loff ? loff[r1] : (int)__umul24(r1, (uint32_t)p)) + sH;
+            o2 = (use_loff ? loff[r2] : (int)__umul24(r2, (uint32_t)p)) + sh;
+            o3 = (use_loff ? loff[r3] : (int)__umul24(r3, (uint32_t)p)) + sTT;
             s1 = sH;
             s2 = sh;
             s3 = sTT;
@@ -791,8 +808,8 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
             const uint32_t d = desc[desc_offset(C, lo) + r];
             const uint32_t tc = (d >> 10) & 1023u;
             s1 = (int)(d >> 20);
-            o0 = loff ? loff[d & 1023u] : (int)(d & 1023u) * p;
-            o1 = (tc == kCarried ? o0 : (loff ? loff[tc] : (int)tc * p)) + s1;
+            o0 = use_loff ? loff[d & 1023u] : (int)__umul24(d & 1023u, (uint32_t)p);
+            o1 = (tc == kCarried ? o0 : (use_loff ? loff[tc] : (int)__umul24(tc, (uint32_t)p))) + s1;
             o2 = tc == kCarried;
         }
     }
@@ -836,6 +853,9 @@ template <int SMAX, int RW>
 __device__ __forceinline__ void write_rows_slots(float* base, float* dummy, const float (&v)[RW][SMAX], int p,
                                                  int lane, uint32_t sw, int nq)
 {
+#if RT_SLOT_OPAQUE_LANE
+    asm volatile("" : "+v"(lane));
+#endif
     const bool tail_ok = lane + 64 * (SMAX - 1) < p;
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
@@ -858,6 +878,9 @@ template <int SMAX, int RW>
 __device__ __forceinline__ void store_rows_slots(const float (&v)[RW][SMAX], int p, int lane, uint32_t sw, int nq,
                                                  __amdgpu_buffer_rsrc_t rs, uint32_t st_o0)
 {
+#if RT_SLOT_OPAQUE_LANE
+    asm volatile("" : "+v"(lane));
+#endif
     const bool tail_ok = lane + 64 * (SMAX - 1) < p;
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
@@ -878,8 +901,10 @@ __device__ __forceinline__ void store_rows_slots(const float (&v)[RW][SMAX], int
 }
 
 // kPack2 merge step (p <= 32; units always with a blob): register row i of
-// a wave holds two output rows, the wave's rows 2i (lanes 0-31) and 2i + 1
-// (lanes 32-63), bin j = lane & 31.  Every lane resolves its own row's
+// wave w holds two adjacent output rows, 2(w + 8i) in lanes 0-31 and
+// 2(w + 8i) + 1 in lanes 32-63, bin j = lane & 31 (adjacent rows: the two
+// halves of a read or write hit disjoint banks -- rows 8 apart, as before,
+// collided on every bank at p = 16 or 32).  Every lane resolves its own row's
 // descriptor (the two halves read different table words; lanes of a half
 // read the same word) and computes its bin's wrapped indices itself: no
 // v_readlane and no per-row scalar work, so a wave instruction does the
@@ -887,7 +912,7 @@ __device__ __forceinline__ void store_rows_slots(const float (&v)[RW][SMAX], int
 // additions of merge_level2_dense; otherwise one level (carried size-1 nodes
 // add -0.0).  Rows past nrows and bins past p compute in-bounds garbage that
 // is never written back.
-template <int RW, bool TWO>
+template <int RW, bool TWO, bool FIRST>
 __device__ __forceinline__ void merge_step_lanes(const UnitCtx& C, const float* src, int p, int lo, int lane, int wave,
                                                  int nrows, float (&v)[RW][1], const int* loff)
 {
@@ -895,26 +920,30 @@ __device__ __forceinline__ void merge_step_lanes(const UnitCtx& C, const float* 
     // the level loop into 2 x RW long-lived registers (spills)
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    const int h = ln >> 5, j = ln & 31;
+    // bins past p read bin 0's words (a broadcast, no extra bank cycles)
+    const int h = ln >> 5, j = (ln & 31) < p ? (ln & 31) : 0;
     const uint32_t* const desc = desc_table(C);
     const int dl = TWO ? 0 : desc_offset(C, lo);
     const uint2* const step = reinterpret_cast<const uint2*>(TWO ? slot_table(C, lo) : C.aux);
     const lds_cptr sp = (lds_cptr)src;
     // groups of G register rows without a branch between them, so the
     // descriptor chains (2-4 dependent LDS reads per row) of a group overlap
-    constexpr int G = 4;
+#ifndef RT_LANES_GROUP
+#define RT_LANES_GROUP 4
+#endif
+    constexpr int G = RT_LANES_GROUP;
     auto row = [&](int i) {
-        int r = wave + kConeWaves * (2 * i + h);
+        int r = 2 * (wave + kConeWaves * i) + h;
         r = r < nrows ? r : nrows - 1;
         if constexpr (TWO) {
             // the host-resolved row: source rows q0..q3 of level lo + 2, rolls
             const uint2 e = step[r];
             const uint32_t q0 = e.x & 1023u, q1 = (e.x >> 10) & 1023u, q2 = (e.x >> 20) & 1023u, q3 = e.y & 1023u;
             const int sH = (int)((e.y >> 10) & 63u), sh = (int)((e.y >> 16) & 63u), sTT = (int)((e.y >> 22) & 63u);
-            const int o0 = loff ? loff[q0] : (int)q0 * p;
-            const int o1 = loff ? loff[q1] : (int)q1 * p;
-            const int o2 = loff ? loff[q2] : (int)q2 * p;
-            const int o3 = loff ? loff[q3] : (int)q3 * p;
+            const int o0 = FIRST ? loff[q0] : (int)__umul24(q0, (uint32_t)p);
+            const int o1 = FIRST ? loff[q1] : (int)__umul24(q1, (uint32_t)p);
+            const int o2 = FIRST ? loff[q2] : (int)__umul24(q2, (uint32_t)p);
+            const int o3 = FIRST ? loff[q3] : (int)__umul24(q3, (uint32_t)p);
             int i1 = j + sH, i2 = j + sh, i3 = j + sTT;
             i1 = i1 >= p ? i1 - p : i1;
             i2 = i2 >= p ? i2 - p : i2;
@@ -929,8 +958,8 @@ __device__ __forceinline__ void merge_step_lanes(const UnitCtx& C, const float* 
             const uint32_t tc = (d >> 10) & 1023u;
             const bool car = tc == kCarried;
             const int sh = (int)(d >> 20);
-            const int ho = loff ? loff[d & 1023u] : (int)(d & 1023u) * p;
-            const int to = car ? ho : (loff ? loff[tc] : (int)tc * p);
+            const int ho = FIRST ? loff[d & 1023u] : (int)__umul24(d & 1023u, (uint32_t)p);
+            const int to = car ? ho : (FIRST ? loff[tc & 1023u] : (int)__umul24(tc, (uint32_t)p));
             int i1 = j + sh;
             i1 = i1 >= p ? i1 - p : i1;
             const float x0 = lds_ld(sp + ho + j);
@@ -941,7 +970,7 @@ __device__ __forceinline__ void merge_step_lanes(const UnitCtx& C, const float* 
     };
 #pragma unroll
     for (int g = 0; g < RW; g += G) {
-        if (wave + kConeWaves * 2 * g < nrows) {
+        if (2 * (wave + kConeWaves * g) < nrows) {
 #pragma unroll
             for (int i = g; i < (g + G < RW ? g + G : RW); ++i) row(i);
         }
@@ -959,9 +988,9 @@ __device__ __forceinline__ void write_rows_lanes(float* base, float* dummy, cons
     const int h = ln >> 5, j = ln & 31;
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
-        if (wave + kConeWaves * 2 * i < nrows) {
-            const int r = wave + kConeWaves * (2 * i + h);
-            *((r < nrows && j < p) ? base + r * p + j : dummy) = v[i][0];
+        if (2 * (wave + kConeWaves * i) < nrows) {
+            const int r = 2 * (wave + kConeWaves * i) + h;
+            *((r < nrows && j < p) ? base + (int)__umul24((uint32_t)r, (uint32_t)p) + j : dummy) = v[i][0];
         }
     }
 }
@@ -977,9 +1006,9 @@ __device__ __forceinline__ void store_rows_lanes(const float (&v)[RW][1], int p,
     const int h = ln >> 5, j = ln & 31;
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
-        if (wave + kConeWaves * 2 * i < nrows) {
-            const int r = wave + kConeWaves * (2 * i + h);
-            const uint32_t o = (r < nrows && j < p) ? st_o0 + (uint32_t)(r * p + j) * 4u : 0x80000000u;
+        if (2 * (wave + kConeWaves * i) < nrows) {
+            const int r = 2 * (wave + kConeWaves * i) + h;
+            const uint32_t o = (r < nrows && j < p) ? st_o0 + (__umul24((uint32_t)r, (uint32_t)p) + (uint32_t)j) * 4u : 0x80000000u;
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][0]), rs, (int)o, 0, 0);
         }
     }
@@ -1017,8 +1046,13 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
             const bool first = l == L - 1;
             const float* src = first ? src0 : base;
             const int* lo_src = first ? loff : nullptr;
-            if (two) merge_step_lanes<RW, true>(C, src, p, lo, lane, wave, nrows, v, lo_src);
-            else merge_step_lanes<RW, false>(C, src, p, lo, lane, wave, nrows, v, lo_src);
+            if (first) {
+                if (two) merge_step_lanes<RW, true, true>(C, src, p, lo, lane, wave, nrows, v, lo_src);
+                else merge_step_lanes<RW, false, true>(C, src, p, lo, lane, wave, nrows, v, lo_src);
+            } else {
+                if (two) merge_step_lanes<RW, true, false>(C, src, p, lo, lane, wave, nrows, v, lo_src);
+                else merge_step_lanes<RW, false, false>(C, src, p, lo, lane, wave, nrows, v, lo_src);
+            }
             l = lo - 1;
             if (lo == 0 && st) {
                 store_rows_lanes<RW>(v, p, lane, wave, nrows, rs, st_o0);
@@ -1042,8 +1076,13 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
                 const int* lo_src = first ? loff : nullptr;
                 uint32_t sw;
                 int nq;
-                if (two) merge_step_slots<SMAX, RW, true>(C, src, p, lo, lane, wave, v, lo_src, sw, nq);
-                else merge_step_slots<SMAX, RW, false>(C, src, p, lo, lane, wave, v, lo_src, sw, nq);
+                if (first || !RT_SLOT_FIRST) {
+                    if (two) merge_step_slots<SMAX, RW, true, true>(C, src, p, lo, lane, wave, v, lo_src, sw, nq);
+                    else merge_step_slots<SMAX, RW, false, true>(C, src, p, lo, lane, wave, v, lo_src, sw, nq);
+                } else {
+                    if (two) merge_step_slots<SMAX, RW, true, false>(C, src, p, lo, lane, wave, v, lo_src, sw, nq);
+                    else merge_step_slots<SMAX, RW, false, false>(C, src, p, lo, lane, wave, v, lo_src, sw, nq);
+                }
                 l = lo - 1;
                 if (lo == 0 && st) {
                     store_rows_slots<SMAX, RW>(v, p, lane, sw, nq, rs, st_o0);
