@@ -1143,6 +1143,13 @@ constexpr int kSnrWin = 12;
 #define RT_SNR_MAX_CHUNK 17
 #endif
 constexpr int kSnrMaxChunk = RT_SNR_MAX_CHUNK;
+// rows per lane and S/N pass for 16-lane row groups (p = 129-272).  A/B
+// (ms per cfg2 trial): 2 rows (one pass per final unit instead of two,
+// independent chains interleaved) 9.13 vs 8.87 -- the doubled register
+// window spills ~37 SGPRs -- so 1.
+#ifndef RT_SNR_ROWS
+#define RT_SNR_ROWS 1
+#endif
 
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v)
@@ -1262,6 +1269,44 @@ __device__ __forceinline__ float window_dispatch(int w, const float (&z)[CH + kS
     }
 }
 
+// the same for two rows at once (independent chains in one block)
+template <int CH, int W>
+__device__ __forceinline__ void window_max2(const float (&z0)[CH + kSnrWin], const float (&c0)[CH],
+                                            const float (&z1)[CH + kSnrWin], const float (&c1)[CH], float& d0,
+                                            float& d1)
+{
+    float m0 = -INFINITY, m1 = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+        m0 = fmaxf(m0, __fsub_rn(z0[i + W], c0[i]));
+        m1 = fmaxf(m1, __fsub_rn(z1[i + W], c1[i]));
+    }
+    d0 = m0;
+    d1 = m1;
+}
+
+template <int CH>
+__device__ __forceinline__ void window_dispatch2(int w, const float (&z0)[CH + kSnrWin], const float (&c0)[CH],
+                                                 const float (&z1)[CH + kSnrWin], const float (&c1)[CH], float& d0,
+                                                 float& d1)
+{
+    switch (w) {
+    case 1: window_max2<CH, 1>(z0, c0, z1, c1, d0, d1); break;
+    case 2: window_max2<CH, 2>(z0, c0, z1, c1, d0, d1); break;
+    case 3: window_max2<CH, 3>(z0, c0, z1, c1, d0, d1); break;
+    case 4: window_max2<CH, 4>(z0, c0, z1, c1, d0, d1); break;
+    case 5: window_max2<CH, 5>(z0, c0, z1, c1, d0, d1); break;
+    case 6: window_max2<CH, 6>(z0, c0, z1, c1, d0, d1); break;
+    case 7: window_max2<CH, 7>(z0, c0, z1, c1, d0, d1); break;
+    case 8: window_max2<CH, 8>(z0, c0, z1, c1, d0, d1); break;
+    case 9: window_max2<CH, 9>(z0, c0, z1, c1, d0, d1); break;
+    case 10: window_max2<CH, 10>(z0, c0, z1, c1, d0, d1); break;
+    case 11: window_max2<CH, 11>(z0, c0, z1, c1, d0, d1); break;
+    case 12: window_max2<CH, 12>(z0, c0, z1, c1, d0, d1); break;
+    default: d0 = d1 = -INFINITY; break;
+    }
+}
+
 #ifdef RT_STAMPS
 #define RT_SNR_MARK(i)                                                           \
     do {                                                                         \
@@ -1271,19 +1316,22 @@ __device__ __forceinline__ float window_dispatch(int w, const float (&z)[CH + kS
 #define RT_SNR_MARK(i) do { } while (0)
 #endif
 
-template <int CH, int G>
+// NR rows per lane and pass (NR = 2: the lane's rows r and r + 512/G are
+// independent chains interleaved in one instruction stream, and half as many
+// row passes -- barriers, DPP scans -- per unit).
+template <int CH, int G, int NR = 1>
 __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, float* data, int q, const int* wl,
                                          int nev, int c, int tid, const float* whb, unsigned long long* tl)
 {
-    constexpr bool kDpp = true;
     const int lane = tid & 63;
     const int p = U.p;
     const int g = lane & (G - 1);
     int j0 = min(g * c, p);
     int cnt = min(j0 + c, p) - j0;                // columns of this lane (may be 0)
     const int owner = (p - 1) / c;
-    const int rows_per_pass = kConeBlock / G;
-    const int writer = kDpp ? G - 1 : 0;
+    constexpr int kRowsPerSet = kConeBlock / G;
+    constexpr int rows_per_pass = NR * kRowsPerSet;
+    constexpr int writer = G - 1;
     const uint32_t nw = a.num_widths;
     float* snr = a.snr + (uint64_t)U.trial * a.snr_stride + (U.snr_row + (uint64_t)U.s0) * (uint64_t)nw;
     const __amdgpu_buffer_rsrc_t srs = buffer_rsrc(snr, (uint32_t)nev * nw * 4u);
@@ -1292,106 +1340,142 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
         // recomputed by one v_cmp each instead of being hoisted out of the
         // loop into SGPR pairs that spill (two v_readlane per use)
         asm volatile("" : "+v"(j0), "+v"(cnt));
-        const int r = base + (tid / G);
-        const bool active = r < nev;
-        float* row = data + min(r, nev - 1) * q + j0;
-        float cp[CH];
+        int r[NR];
+        bool active[NR];
+        float* row[NR];
+        float cp[NR][CH];
+        double part[NR];
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+            r[k] = base + k * kRowsPerSet + (tid / G);
+            active[k] = r[k] < nev;
+            row[k] = data + min(r[k], nev - 1) * q + j0;
+        }
         // every lane reads CH columns at immediate offsets (past its chunk:
         // the next chunk, the next row or the LDS pad), masked to 0
 #pragma unroll
-        for (int i = 0; i < CH; ++i) {
-            const float x = row[i];
-            cp[i] = i < cnt ? x : 0.0f;
-        }
+        for (int k = 0; k < NR; ++k)
+#pragma unroll
+            for (int i = 0; i < CH; ++i) {
+                const float x = row[k][i];
+                cp[k][i] = i < cnt ? x : 0.0f;
+            }
         // fp64 prefix: the masked columns add +0.0 (the partial sums start at
         // +0.0 and are never -0.0, so the additions are exact no-ops)
-        double part = 0.0;
 #pragma unroll
-        for (int i = 0; i < CH; ++i) part = part + (double)cp[i];
-        double acc;
-        if constexpr (kDpp) {
-            const double incl = seg_scan_dpp<G>(part, lane);
-            acc = dpp_d<0x138>(incl);               // wave_shr:1 -- lane g takes lane g - 1
-        } else {
-            double incl = part;
-            for (int d = 1; d < G; d <<= 1) {
-                const double y = __shfl_up(incl, d, G);
-                if (g >= d) incl += y;
+        for (int k = 0; k < NR; ++k) part[k] = 0.0;
+#pragma unroll
+        for (int i = 0; i < CH; ++i)
+#pragma unroll
+            for (int k = 0; k < NR; ++k) part[k] = part[k] + (double)cp[k][i];
+        double acc[NR];
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+            const double incl = seg_scan_dpp<G>(part[k], lane);
+            acc[k] = dpp_d<0x138>(incl);              // wave_shr:1 -- lane g takes lane g - 1
+            if (g == 0) acc[k] = 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < CH; ++i)
+#pragma unroll
+            for (int k = 0; k < NR; ++k) {
+                acc[k] = acc[k] + (double)cp[k][i];
+                cp[k][i] = (float)acc[k];
             }
-            acc = __shfl_up(incl, 1, G);
-        }
-        if (g == 0) acc = 0.0;
+        float sum[NR];
 #pragma unroll
-        for (int i = 0; i < CH; ++i) {
-            acc = acc + (double)cp[i];
-            cp[i] = (float)acc;
-        }
-        const float sum = __shfl((float)acc, owner, G);
+        for (int k = 0; k < NR; ++k) sum[k] = __shfl((float)acc[k], owner, G);
         {
             // columns past the lane's chunk (and rows past nev) go to a dummy
             // word in the LDS pad: an address select instead of exec masks
             float* const dummy = data + kLdsDataFloats + 4 + lane;
 #pragma unroll
-            for (int i = 0; i < CH; ++i) *((active && i < cnt) ? row + i : dummy) = cp[i];
+            for (int k = 0; k < NR; ++k)
+#pragma unroll
+                for (int i = 0; i < CH; ++i) *((active[k] && i < cnt) ? row[k] + i : dummy) = cp[k][i];
         }
 #pragma unroll
-        for (int i = 0; i < CH; ++i) cp[i] = i < cnt ? cp[i] : INFINITY;
+        for (int k = 0; k < NR; ++k)
+#pragma unroll
+            for (int i = 0; i < CH; ++i) cp[k][i] = i < cnt ? cp[k][i] : INFINITY;
         RT_SNR_MARK(7);
         lds_barrier();                        // prefix rows visible to all lanes
         RT_SNR_MARK(8);
-        const float* crow = data + min(r, nev - 1) * q;
-        // one lane per row stores; the others store out of the buffer's
-        // range, which drops them (no exec-mask save/restore)
-        const uint32_t so = (active && g == writer) ? (uint32_t)r * nw * 4u : 0x80000000u;
-        auto emit = [&](uint32_t iw, int w, float dmax) {
-            (void)w;
-            dmax = seg_max_dpp<G>(dmax, lane);
+        const float* crow[NR];
+        uint32_t so[NR];
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+            crow[k] = data + min(r[k], nev - 1) * q;
+            // one lane per row stores; the others store out of the buffer's
+            // range, which drops them (no exec-mask save/restore)
+            so[k] = (active[k] && g == writer) ? (uint32_t)r[k] * nw * 4u : 0x80000000u;
+        }
+        auto emit = [&](uint32_t iw, const float (&dmax)[NR]) {
             // h + b and b of this width (per unit, in LDS: uniform reads)
             const float hpb = __int_as_float(uni(__float_as_int(whb[2 * iw])));
             const float b = __int_as_float(uni(__float_as_int(whb[2 * iw + 1])));
-            const float v = (hpb * dmax - b * sum) / U.stdnoise;
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srs, (int)(so + iw * 4u), 0, 0);
+#pragma unroll
+            for (int k = 0; k < NR; ++k) {
+                const float dm = seg_max_dpp<G>(dmax[k], lane);
+                const float v = (hpb * dm - b * sum[k]) / U.stdnoise;
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srs, (int)(so[k] + iw * 4u), 0, 0);
+            }
         };
         if constexpr (CH <= kSnrMaxChunk) {
             // widths <= kSnrWin from the register window c[j0 .. j0 + CH + kSnrWin)
-            float z[CH + kSnrWin];
-            {
+            float z[NR][CH + kSnrWin];
+#pragma unroll
+            for (int k = 0; k < NR; ++k) {
                 // two opaque bases (row and row - p), slot offsets immediate
-                lds_cptr za = (lds_cptr)(crow + j0);
+                lds_cptr za = (lds_cptr)(crow[k] + j0);
                 lds_cptr zb = za - p;
                 asm("" : "+v"(za), "+v"(zb));
 #pragma unroll
-                for (int k = 0; k < CH + kSnrWin; ++k) {
-                    const bool wrap = j0 + k >= p;
-                    const float va = za[k], vb = zb[k];
-                    z[k] = wrap ? __fadd_rn(vb, sum) : va;
+                for (int t = 0; t < CH + kSnrWin; ++t) {
+                    const bool wrap = j0 + t >= p;
+                    const float va = za[t], vb = zb[t];
+                    z[k][t] = wrap ? __fadd_rn(vb, sum[k]) : va;
                 }
             }
             RT_SNR_MARK(9);
             for (uint32_t iw = 0; iw < nw; ++iw) {
                 const int w = uni(wl[iw]);
-                if (w <= kSnrWin) emit(iw, w, window_dispatch<CH>(w, z, cp));
+                if (w <= kSnrWin) {
+                    float dm[NR];
+#pragma unroll
+                    for (int k = 0; k < NR; ++k) dm[k] = -INFINITY;
+                    if constexpr (NR == 1) {
+                        dm[0] = window_dispatch<CH>(w, z[0], cp[0]);
+                    } else {
+                        window_dispatch2<CH>(w, z[0], cp[0], z[1], cp[1], dm[0], dm[1]);
+                    }
+                    emit(iw, dm);
+                }
             }
         }
         // wider widths: the window c[j0 + w ..] read from LDS per width
         for (uint32_t iw = 0; iw < nw; ++iw) {
             const int w = uni(wl[iw]);
             if (CH <= kSnrMaxChunk && w <= kSnrWin) continue;
-            float dmax = -INFINITY;
+            float dmax[NR];
             const int last = max(cnt - 1, 0);
-            float lv[CH];
 #pragma unroll
-            for (int t = 0; t < CH; ++t) {
-                const int k = j0 + min(t, last) + w;
-                lv[t] = crow[k >= p ? k - p : k];
-            }
+            for (int k = 0; k < NR; ++k) {
+                dmax[k] = -INFINITY;
+                float lv[CH];
 #pragma unroll
-            for (int i = 0; i < CH; ++i) {
-                const bool wrap = j0 + min(i, last) + w >= p;
-                const float ck = wrap ? __fadd_rn(lv[i], sum) : lv[i];
-                dmax = fmaxf(dmax, __fsub_rn(ck, cp[i]));  // diff_max, kernels.hpp:50-60
+                for (int t = 0; t < CH; ++t) {
+                    const int j = j0 + min(t, last) + w;
+                    lv[t] = crow[k][j >= p ? j - p : j];
+                }
+#pragma unroll
+                for (int i = 0; i < CH; ++i) {
+                    const bool wrap = j0 + min(i, last) + w >= p;
+                    const float ck = wrap ? __fadd_rn(lv[i], sum[k]) : lv[i];
+                    dmax[k] = fmaxf(dmax[k], __fsub_rn(ck, cp[k][i]));  // diff_max, kernels.hpp:50-60
+                }
             }
-            emit(iw, w, dmax);
+            emit(iw, dmax);
         }
         RT_SNR_MARK(10);
     }
@@ -1451,7 +1535,7 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
         }
         if constexpr (variant_has_group(SMAX, 16)) {
             if (G == 16) {
-                snr_rows<kSnrMaxChunk, 16>(a, U, data, q, wl, nev, c, tid, whb, tl);
+                snr_rows<kSnrMaxChunk, 16, RT_SNR_ROWS>(a, U, data, q, wl, nev, c, tid, whb, tl);
                 return;
             }
         }
