@@ -84,6 +84,12 @@ enum : int {
 // row A | row B << 10 | kind << 20.
 enum : uint32_t { kSlotOne = 0, kSlotTwo = 1, kSlotPair = 2 };
 constexpr int kSlotWords = kConeWgsPerCu == 4 ? 288 : 544;   // LDS area of a unit's slot tables
+// 4/5-slot variants (p = 193-320, rows <= 72 per unit): slot tables with
+// every row resolved (build_tile_blob), 16 bytes per row: source-row LDS
+// offsets (16 bits each), the three rolls (10 bits each, | carried << 30 for
+// single steps) and the slot word
+RT_HD constexpr bool resolved_slots(int smax) { return smax == 4 || smax == 5; }
+constexpr int kAuxMetaWords = kBlobHeader + kDescEntries + kMaxRows + kSlotWords;   // the metadata area
 constexpr uint32_t kNoBlob = 0xFFFFFFFFu;
 constexpr uint32_t kCarriedRow = 1023;
 // 16-byte chunks of a unit's LDS DMA fill (setup_unit): a whole unit's block

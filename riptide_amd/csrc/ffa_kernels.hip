@@ -780,6 +780,28 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
     nq = uni(ns > wave ? (ns - wave + kConeWaves - 1) / kConeWaves : 0);
     // lane i < 32 resolves row A of the wave's slot i, lane 32 + i its row B
     const int qi = lane & 31;
+    int o0 = 0, o1 = 0, o2 = 0, o3 = 0, s1 = 0, s2 = 0, s3 = 0;
+    if constexpr (resolved_slots(SMAX)) {
+        // host-resolved rows: one 16-byte entry per lane (the slot's row A in
+        // lanes 0-31 with the slot word, row B in lanes 32-63); lanes past
+        // the wave's slots read in-bounds words that are never used
+        const uint4 e = reinterpret_cast<const uint4*>(st)[1 + 2 * (wave + kConeWaves * qi) + (lane >> 5)];
+        sw = lane < 32 ? e.w : 0u;
+        s1 = (int)(e.z & 1023u);
+        if constexpr (TWO) {
+            s2 = (int)((e.z >> 10) & 1023u);
+            s3 = (int)((e.z >> 20) & 1023u);
+            o0 = (int)(e.x & 0xFFFFu);
+            o1 = (int)(e.x >> 16) + s1;
+            o2 = (int)(e.y & 0xFFFFu) + s2;
+            o3 = (int)(e.y >> 16) + s3;
+        } else {
+            o0 = (int)(e.x & 0xFFFFu);
+            o1 = (int)(e.x >> 16) + s1;
+            o2 = (int)((e.z >> 30) & 1u);
+        }
+        (void)loff;
+    } else {
     sw = qi < nq ? st[1 + wave + kConeWaves * qi] : 0u;
     const bool act = qi < nq && (lane < 32 || (sw >> 20) == kSlotTwo);
     const int r = lane < 32 ? (int)(sw & 1023u) : (int)((sw >> 10) & 1023u);
@@ -787,7 +809,6 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
     // the first step reads the bottom level through its row offsets: a
     // template constant (a run-time test of loff made every offset a branch)
     const bool use_loff = RT_SLOT_FIRST ? FIRST : loff != nullptr;
-    int o0 = 0, o1 = 0, o2 = 0, o3 = 0, s1 = 0, s2 = 0, s3 = 0;
     if (act) {
         if constexpr (TWO) {
             const uint32_t d0 = desc[desc_offset(C, lo) + r];
@@ -812,6 +833,7 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
             o1 = (tc == kCarried ? o0 : (use_loff ? loff[tc] : (int)__umul24(tc, (uint32_t)p))) + s1;
             o2 = tc == kCarried;
         }
+    }
     }
     const lds_cptr l1 = (lds_cptr)src + lane;
     const int jl = p - 1 - 64 * (SMAX - 1);   // lane of bin p - 1 in the last slot

@@ -401,12 +401,14 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
     // launch's whole batch)
     std::vector<int> slot_rw(out.items.size(), 0);
     std::vector<bool> packed(out.items.size(), false);
+    std::vector<int> smax_of(out.items.size(), 0);
     for (const Launch& L : out.launches) {
         // row-slot tables for the kernel instances that use them (SMAX <= 5)
         const int rw = L.smax <= 5 ? (L.rw ? (int)L.rw : merge_rows_per_wave((int)L.smax)) : 0;
         for (uint32_t i = L.first; i < L.first + L.count; ++i) {
             slot_rw[i] = rw;
             packed[i] = L.smax == (uint32_t)kPack2;
+            smax_of[i] = (int)L.smax;
         }
     }
     for (size_t i = 0; i < out.items.size(); ++i) {
@@ -419,7 +421,7 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
             ((uint64_t)it.levels * it.node_size > (uint64_t)kDescEntries || it.node_size > (uint32_t)kMaxRows))
             continue;
         it.pad = (uint32_t)out.blob.size();
-        build_tile_blob(it, out.xf[it.xform].p, slot_rw[i], packed[i], out.blob);
+        build_tile_blob(it, out.xf[it.xform].p, slot_rw[i], smax_of[i], out.blob);
     }
     validate_exec_plan(out, snr_epilogue);
 }
@@ -480,8 +482,10 @@ static void build_row_slots(const uint32_t* d, uint32_t n, uint32_t p, int rw, s
     }
 }
 
-void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, bool packed, std::vector<uint32_t>& out)
+void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, int smax, std::vector<uint32_t>& out)
 {
+    const bool packed = smax == kPack2;
+    const bool resolved = slot_rw > 0 && resolved_slots(smax);
     struct R { uint32_t size, lo, hi; uint32_t start; uint32_t base; };
     const int L = it.levels;
     const bool tile = it.mode == kModeTile;
@@ -566,6 +570,25 @@ void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, bool packed, s
             desc[doff[l] + r] = h | (t << 10) | (sh << 20);
         }
     }
+    // bottom level: one DMA run per range, each at its own 16-byte phase,
+    // consecutive in LDS; issued as segments of <= 64 16-byte chunks (one
+    // LDS-DMA wave instruction each: LDS chunk c0, chunks n, source chunk g)
+    std::vector<uint32_t> loff_v(nb), segs;
+    uint32_t cb = 0;
+    for (uint32_t ri = 0; ri < nruns; ++ri) {
+        const R& g = lv[L][ri];
+        const uint32_t first = (g.start + g.lo) * p;
+        const uint32_t al = first & 3u, cnt = g.hi - g.lo + 1;
+        const uint32_t nch = (cnt * p + al + 3) >> 2;
+        for (uint32_t r = 0; r < cnt; ++r) loff_v[g.base + r] = 4 * cb + al + r * p;
+        for (uint32_t c = 0; c < nch; c += 64) {
+            segs.push_back(cb + c);
+            segs.push_back(std::min<uint32_t>(64u, nch - c));
+            segs.push_back((first - al) / 4 + c);
+            segs.push_back(0u);
+        }
+        cb += nch;
+    }
     // row slots of every merge step (the kernel's step order: two levels per
     // step where no level below the output holds size-1 nodes)
     std::vector<uint32_t> slot_area;
@@ -613,6 +636,55 @@ void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, bool packed, s
         const uint32_t base = base0 + (base0 & 1u);
         for (int l = 0; l <= L; ++l)
             if (fused[l]) slot_off[l] = base + rel[l];
+    } else if (resolved) {
+        // 4/5-slot variants: every step's row slots with their rows resolved
+        // (resolved_slots): a lane reads its slot's row A (lanes 0-31) or row
+        // B (32-63) as one 16-byte entry -- LDS offsets of the source rows
+        // (the first step's in the fill layout), the rolls and the slot word
+        // -- instead of a chain of descriptor reads; the descriptor table is
+        // not stored.
+        std::vector<uint32_t> sl;
+        const uint32_t base0 = kBlobHeader + nb;
+        const uint32_t base = (base0 + 3u) & ~3u;       // 16-byte aligned tables
+        slot_area.assign(base - base0, 0u);
+        for (int l = L - 1; l >= 0;) {
+            const bool two = l >= 1 && (tile || (it.node_size >> l) >= 2);
+            const int lo = two ? l - 1 : l;
+            const bool first = l == L - 1;
+            build_row_slots(desc + doff[lo], nrows[lo], p, slot_rw, sl);
+            slot_off[lo] = (uint32_t)(base0 + slot_area.size());
+            slot_area.insert(slot_area.end(), {(uint32_t)sl.size(), 0u, 0u, 0u});
+            auto off = [&](uint32_t row) { return first ? loff_v[row] : row * p; };
+            auto entry = [&](uint32_t r, uint32_t* e) {
+                const uint32_t d0 = desc[doff[lo] + r];
+                if (two) {
+                    const uint32_t dh = desc[doff[lo + 1] + (d0 & 1023u)];
+                    const uint32_t dt = desc[doff[lo + 1] + ((d0 >> 10) & 1023u)];
+                    const uint32_t sh = d0 >> 20, sH = dh >> 20, sTT = ((d0 >> 20) + (dt >> 20)) % p;
+                    e[0] = off(dh & 1023u) | (off((dh >> 10) & 1023u) << 16);
+                    e[1] = off(dt & 1023u) | (off((dt >> 10) & 1023u) << 16);
+                    e[2] = sH | (sh << 10) | (sTT << 20);
+                } else {
+                    const uint32_t tc = (d0 >> 10) & 1023u, car = tc == kCarriedRow;
+                    const uint32_t oh = off(d0 & 1023u);
+                    e[0] = oh | ((car ? oh : off(tc)) << 16);
+                    e[1] = 0u;
+                    e[2] = (d0 >> 20) | (car << 30);
+                }
+            };
+            for (uint32_t sw : sl) {
+                uint32_t e[8] = {};
+                entry(sw & 1023u, e);
+                e[3] = sw;
+                if ((sw >> 20) == kSlotTwo) entry((sw >> 10) & 1023u, e + 4);
+                slot_area.insert(slot_area.end(), e, e + 8);
+            }
+            l = lo - 1;
+        }
+        if (slot_area.size() > (size_t)(kAuxMetaWords - kBlobHeader - nb))
+            throw std::runtime_error("schedule: resolved row-slot tables exceed their LDS area");
+        entries = 0;   // no descriptor table in LDS
+        for (int l = 0; l <= L; ++l) doff[l] = 0;
     } else if (slot_rw > 0) {
         std::vector<uint32_t> sl;
         for (int l = L - 1; l >= 0;) {
@@ -625,25 +697,6 @@ void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, bool packed, s
             l = lo - 1;
         }
         if (slot_area.size() > (size_t)kSlotWords) throw std::runtime_error("schedule: row-slot tables exceed their LDS area");
-    }
-    // bottom level: one DMA run per range, each at its own 16-byte phase,
-    // consecutive in LDS; issued as segments of <= 64 16-byte chunks (one
-    // LDS-DMA wave instruction each: LDS chunk c0, chunks n, source chunk g)
-    std::vector<uint32_t> loff_v(nb), segs;
-    uint32_t cb = 0;
-    for (uint32_t ri = 0; ri < nruns; ++ri) {
-        const R& g = lv[L][ri];
-        const uint32_t first = (g.start + g.lo) * p;
-        const uint32_t al = first & 3u, cnt = g.hi - g.lo + 1;
-        const uint32_t nch = (cnt * p + al + 3) >> 2;
-        for (uint32_t r = 0; r < cnt; ++r) loff_v[g.base + r] = 4 * cb + al + r * p;
-        for (uint32_t c = 0; c < nch; c += 64) {
-            segs.push_back(cb + c);
-            segs.push_back(std::min<uint32_t>(64u, nch - c));
-            segs.push_back((first - al) / 4 + c);
-            segs.push_back(0u);
-        }
-        cb += nch;
     }
     const uint32_t nsegs = (uint32_t)(segs.size() / 4);
     if (nsegs > (uint32_t)(kConeWaves * 64)) throw std::runtime_error("schedule: unit fill exceeds the DMA segment table");
@@ -663,7 +716,7 @@ void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, bool packed, s
     w[kHdrSlotWords] = (uint32_t)slot_area.size();
     w[kHdrRunOff] = (uint32_t)runoff;
     w[kHdrFill] = cb;
-    std::copy(desc_v.begin(), desc_v.end(), w + kBlobHeader);
+    if (entries) std::copy(desc_v.begin(), desc_v.begin() + entries, w + kBlobHeader);
     std::copy(loff_v.begin(), loff_v.end(), w + kBlobHeader + entries);
     std::copy(slot_area.begin(), slot_area.end(), w + kBlobHeader + entries + nb);
     std::copy(segs.begin(), segs.end(), w + runoff);
@@ -690,7 +743,7 @@ static void validate_blob(const ConeItem& it, uint32_t p, int smax, int rw, cons
     }
     if (c != fill) throw std::runtime_error("schedule: DMA segments do not tile the fill");
     const uint32_t* desc = w + kBlobHeader;
-    if (smax != kPack2)
+    if (smax != kPack2 && !(resolved_slots(smax) && slot_words))
         for (uint32_t l = 0; l < L; ++l)
             if (w[kHdrDesc + l] + w[kHdrRows + l] > entries) throw std::runtime_error("schedule: descriptor table overrun");
     const bool tile = it.mode == kModeTile;
@@ -718,6 +771,42 @@ static void validate_blob(const ConeItem& it, uint32_t p, int smax, int rw, cons
     }
     if (!slot_words) {
         if (smax <= 5 && L > 0) throw std::runtime_error("schedule: unit without row-slot tables");
+        return;
+    }
+    if (resolved_slots(smax)) {
+        const int Q = (rw + 1) / 2;
+        for (int l = (int)L - 1; l >= 0;) {
+            const bool two = l >= 1 && (tile || (it.node_size >> l) >= 2);
+            const int lo = two ? l - 1 : l;
+            const uint32_t n = w[kHdrRows + lo], so = w[kHdrSlotOff + lo];
+            if ((so & 3u) || so < (uint32_t)kBlobHeader + nb || so + 4 > runoff)
+                throw std::runtime_error("schedule: row-slot table outside the blob");
+            const uint32_t ns = w[so];
+            if (ns > (uint32_t)(kConeWaves * Q) || so + 4 + 8 * ns > runoff) throw std::runtime_error("schedule: row-slot table overrun");
+            std::vector<uint8_t> seen(n, 0);
+            auto check_entry = [&](const uint32_t* e) {
+                const uint32_t s1 = e[2] & 1023u, s2 = (e[2] >> 10) & 1023u, s3 = (e[2] >> 20) & 1023u;
+                const uint32_t top = (uint32_t)kLdsBufFloats;
+                if (s1 >= p || (two && (s2 >= p || s3 >= p)) || (e[0] & 0xFFFFu) + p > top ||
+                    (e[0] >> 16) + p > top || (two && ((e[1] & 0xFFFFu) + p > top || (e[1] >> 16) + p > top)))
+                    throw std::runtime_error("schedule: bad resolved row entry");
+            };
+            for (uint32_t g = 0; g < ns; ++g) {
+                const uint32_t* e = w + so + 4 + 8 * g;
+                const uint32_t sw = e[3], ra = sw & 1023u, rb = (sw >> 10) & 1023u, kind = sw >> 20;
+                const int q = (int)g / kConeWaves;
+                const bool two_rows = kind == kSlotTwo || kind == kSlotPair;
+                if (kind > kSlotPair || ra >= n || (two_rows && (rb >= n || 2 * q + 1 >= rw)) ||
+                    (kind == kSlotPair && rb != ra + 1))
+                    throw std::runtime_error("schedule: bad row slot");
+                if (seen[ra]++ || (two_rows && seen[rb]++)) throw std::runtime_error("schedule: row slot covers a row twice");
+                check_entry(e);
+                if (kind == kSlotTwo) check_entry(e + 4);
+            }
+            for (uint32_t r = 0; r < n; ++r)
+                if (!seen[r]) throw std::runtime_error("schedule: row-slot table misses a row");
+            l = lo - 1;
+        }
         return;
     }
     const int Q = (rw + 1) / 2;

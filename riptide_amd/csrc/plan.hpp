@@ -87,7 +87,10 @@ struct ExecPlan {
 // gets a table of its output rows pre-resolved (2 words per row: the four
 // source rows, the three rolls) and the descriptor table keeps only the
 // levels single steps read.
-void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, bool packed, std::vector<uint32_t>& out);
+// Resolved slot tables (4/5-slot variants, resolved_slots): per slot two
+// 16-byte entries (row A, row B) of source-row LDS offsets, rolls and the
+// slot word; no descriptor table.
+void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, int smax, std::vector<uint32_t>& out);
 
 // Schedule a list of transforms (p, m, rows_eval, src_off, snr_row, stdnoise
 // filled in by the caller).  With snr_epilogue the last pass of every
