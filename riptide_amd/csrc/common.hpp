@@ -47,22 +47,23 @@ static_assert(kConeBuffers == 1 || kConeBuffers == 2, "RT_CONE_BUFFERS is 1 or 2
 #ifndef RT_CONE_WGS
 #define RT_CONE_WGS 2
 #endif
-static_assert(RT_CONE_WGS == 2 || RT_CONE_WGS == 4, "RT_CONE_WGS is 2 or 4");
+static_assert(RT_CONE_WGS >= 2 && RT_CONE_WGS <= 4, "RT_CONE_WGS is 2, 3 or 4");
 constexpr int kConeWgsPerCu = kConeBuffers == 2 ? 1 : RT_CONE_WGS;
 constexpr int kConeBlock = kConeBuffers == 2 ? 1024 : (kConeWgsPerCu == 2 ? 512 : 256);
+static_assert(kConeBlock % 64 == 0, "whole waves");
 constexpr int kConeWaves = kConeBlock / 64;
 constexpr int kConeWavesPerSimd = kConeWgsPerCu * kConeWaves / 4;
-constexpr int kLdsBufFloats = kConeBuffers == 2 ? 17920 : (kConeWgsPerCu == 2 ? 18176 : 8704);   // one level buffer: a unit's fill (16-byte chunks, runs per range)
+constexpr int kLdsBufFloats = kConeBuffers == 2 ? 17920 : (kConeWgsPerCu == 2 ? 18176 : (kConeWgsPerCu == 3 ? 11712 : 8704));   // one level buffer: a unit's fill (16-byte chunks, runs per range)
 constexpr int kLdsDataFloats = kLdsBufFloats - 256;   // rows x p of any level (the rest: per-range 16-byte phase slack)
 constexpr int kLdsPadFloats = 128;          // slack read (never used) by the unused slots of the last row
-constexpr int kMaxRows = kConeWgsPerCu == 4 ? 192 : 384;          // rows per level (row-offset table, descriptors)
-constexpr int kDescEntries = kConeWgsPerCu == 4 ? 512 : 1024;     // row-descriptor table (all levels of a unit)
+constexpr int kMaxRows = kConeWgsPerCu == 4 ? 192 : (kConeWgsPerCu == 3 ? 256 : 384);          // rows per level (row-offset table, descriptors)
+constexpr int kDescEntries = kConeWgsPerCu == 4 ? 512 : (kConeWgsPerCu == 3 ? 768 : 1024);     // row-descriptor table (all levels of a unit)
 constexpr int kMaxTileLevels = 6;           // L for tile items
 constexpr int kMaxLevels = 11;              // merge levels of any unit (whole units: ceil(log2(kMaxRows)))
 constexpr int kMaxRanges = (1 << (kMaxTileLevels + 1)) - 1;
 constexpr int kMaxWidths = 32;              // boxcar widths handled by the fused S/N epilogue
 constexpr int kSnrChunk = 17;               // S/N epilogue: columns per lane held in registers
-constexpr int kStageRegs = kConeBuffers == 2 ? 25 : 45;   // merge: staged values per lane (rows x slots)
+constexpr int kStageRegs = kConeBuffers == 2 ? 25 : (kConeWgsPerCu == 3 ? 60 : 45);   // merge: staged values per lane (rows x slots)
 constexpr int kMaxSlots = 45;               // merge: 64-bin slots per row (p <= 2880)
 constexpr int kMaxRowsPerWave = 24;         // merge: staged rows per wave
 // header words of a unit's host-built blob (plan.hpp build_tile_blob); a
@@ -133,7 +134,7 @@ RT_HD constexpr int row_pack(int smax) { return smax == kPack2 ? 2 : 1; }
 // (5 x 16 waves = 80 >= 17664 / 221) or at p >= 240 (9 x 8 waves = 72 >=
 // 16128 / 240)
 #ifndef RT_RW4
-#define RT_RW4 (kConeBuffers == 2 ? 5 : 9)
+#define RT_RW4 (kConeBuffers == 2 ? 5 : (kConeWgsPerCu == 3 ? 12 : 9))
 #endif
 RT_HD constexpr int merge_rows_per_wave(int smax)
 {
