@@ -783,9 +783,11 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
     int o0 = 0, o1 = 0, o2 = 0, o3 = 0, s1 = 0, s2 = 0, s3 = 0;
     if constexpr (resolved_slots(SMAX)) {
         // host-resolved rows: one 16-byte entry per lane (the slot's row A in
-        // lanes 0-31 with the slot word, row B in lanes 32-63); lanes past
-        // the wave's slots read in-bounds words that are never used
-        const uint4 e = reinterpret_cast<const uint4*>(st)[1 + 2 * (wave + kConeWaves * qi) + (lane >> 5)];
+        // lanes 0-31 with the slot word, row B in lanes 32-63)
+        // wave-major halves (build_tile_blob): the 32 lanes of a half read
+        // consecutive 16-byte entries; lanes past Q re-read entry Q - 1
+        const int qc = qi < Q ? qi : Q - 1;
+        const uint4 e = reinterpret_cast<const uint4*>(st)[1 + (lane >> 5) * (kConeWaves * Q) + wave * Q + qc];
         sw = lane < 32 ? e.w : 0u;
         s1 = (int)(e.z & 1023u);
         if constexpr (TWO) {

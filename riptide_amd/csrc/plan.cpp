@@ -672,12 +672,21 @@ void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, int smax, std:
                     e[2] = (d0 >> 20) | (car << 30);
                 }
             };
-            for (uint32_t sw : sl) {
-                uint32_t e[8] = {};
-                entry(sw & 1023u, e);
-                e[3] = sw;
-                if ((sw >> 20) == kSlotTwo) entry((sw >> 10) & 1023u, e + 4);
-                slot_area.insert(slot_area.end(), e, e + 8);
+            // wave-major halves: row A entries of wave w's slots q at
+            // [w Q + q], row B entries at [8 Q + w Q + q] (16 bytes each), so
+            // the 32 lanes of a half read consecutive entries (no bank
+            // conflicts; slot g = w + 8 q is the wave's q-th slot)
+            const int Q = (slot_rw + 1) / 2;
+            const size_t t0 = slot_area.size();
+            slot_area.resize(t0 + 4 * 2 * (size_t)kConeWaves * Q, 0u);
+            for (size_t g = 0; g < sl.size(); ++g) {
+                const uint32_t sw = sl[g];
+                const size_t wq = (g % kConeWaves) * Q + g / kConeWaves;
+                uint32_t* ea = slot_area.data() + t0 + 4 * wq;
+                uint32_t* eb = slot_area.data() + t0 + 4 * ((size_t)kConeWaves * Q + wq);
+                entry(sw & 1023u, ea);
+                ea[3] = sw;
+                if ((sw >> 20) == kSlotTwo) entry((sw >> 10) & 1023u, eb);
             }
             l = lo - 1;
         }
@@ -782,7 +791,8 @@ static void validate_blob(const ConeItem& it, uint32_t p, int smax, int rw, cons
             if ((so & 3u) || so < (uint32_t)kBlobHeader + nb || so + 4 > runoff)
                 throw std::runtime_error("schedule: row-slot table outside the blob");
             const uint32_t ns = w[so];
-            if (ns > (uint32_t)(kConeWaves * Q) || so + 4 + 8 * ns > runoff) throw std::runtime_error("schedule: row-slot table overrun");
+            if (ns > (uint32_t)(kConeWaves * Q) || so + 4 + 8 * (uint32_t)(kConeWaves * Q) > runoff)
+                throw std::runtime_error("schedule: row-slot table overrun");
             std::vector<uint8_t> seen(n, 0);
             auto check_entry = [&](const uint32_t* e) {
                 const uint32_t s1 = e[2] & 1023u, s2 = (e[2] >> 10) & 1023u, s3 = (e[2] >> 20) & 1023u;
@@ -792,7 +802,9 @@ static void validate_blob(const ConeItem& it, uint32_t p, int smax, int rw, cons
                     throw std::runtime_error("schedule: bad resolved row entry");
             };
             for (uint32_t g = 0; g < ns; ++g) {
-                const uint32_t* e = w + so + 4 + 8 * g;
+                const uint32_t wq = (g % kConeWaves) * (uint32_t)Q + g / kConeWaves;
+                const uint32_t* e = w + so + 4 + 4 * wq;
+                const uint32_t* eb = w + so + 4 + 4 * ((uint32_t)(kConeWaves * Q) + wq);
                 const uint32_t sw = e[3], ra = sw & 1023u, rb = (sw >> 10) & 1023u, kind = sw >> 20;
                 const int q = (int)g / kConeWaves;
                 const bool two_rows = kind == kSlotTwo || kind == kSlotPair;
@@ -801,7 +813,7 @@ static void validate_blob(const ConeItem& it, uint32_t p, int smax, int rw, cons
                     throw std::runtime_error("schedule: bad row slot");
                 if (seen[ra]++ || (two_rows && seen[rb]++)) throw std::runtime_error("schedule: row slot covers a row twice");
                 check_entry(e);
-                if (kind == kSlotTwo) check_entry(e + 4);
+                if (kind == kSlotTwo) check_entry(eb);
             }
             for (uint32_t r = 0; r < n; ++r)
                 if (!seen[r]) throw std::runtime_error("schedule: row-slot table misses a row");
