@@ -379,11 +379,13 @@ __device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t u, uin
 #endif
         if (ok && dma) {
             // DMA segments: wave w issues segments w, w + 8, ...; its lane i
-            // holds segment w + 8i (one vector load)
+            // holds segment w + 8i (one coalesced vector load)
             const uint4* const segs = reinterpret_cast<const uint4*>(a.blob + U.blob + words);
             const int mine = uni(C.nruns > wave ? (C.nruns - wave + kConeWaves - 1) / kConeWaves : 0);
             uint4 sv = make_uint4(0u, 0u, 0u, 0u);
-            if (lane < mine) sv = segs[wave + kConeWaves * lane];
+            // wave-major table (build_tile_blob): the wave's segments are consecutive
+            const int K = (C.nruns + kConeWaves - 1) / kConeWaves;
+            if (lane < mine) sv = segs[wave * K + lane];
             // the blob's LDS part: the last wave
             const __amdgpu_buffer_rsrc_t rb = buffer_rsrc(a.blob + U.blob, (uint32_t)words * 4u);
             if (wave == kConeWaves - 1) dma_run(rb, 0u, words >> 2, (float*)const_cast<uint32_t*>(C.aux), 0, 1, lane);

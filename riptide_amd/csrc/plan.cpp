@@ -708,6 +708,16 @@ void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, int smax, std:
         if (slot_area.size() > (size_t)kSlotWords) throw std::runtime_error("schedule: row-slot tables exceed their LDS area");
     }
     const uint32_t nsegs = (uint32_t)(segs.size() / 4);
+    {
+        // wave-major order: segment g (issued by wave g % 8) at
+        // (g % 8) * K + g / 8, K = ceil(nsegs / 8), so a wave's lanes load
+        // its segments from consecutive 16-byte entries
+        const uint32_t K = (nsegs + kConeWaves - 1) / kConeWaves;
+        std::vector<uint32_t> wm((size_t)4 * K * kConeWaves, 0u);
+        for (uint32_t g = 0; g < nsegs; ++g)
+            std::copy(segs.begin() + 4 * g, segs.begin() + 4 * g + 4, wm.begin() + 4 * ((g % kConeWaves) * K + g / kConeWaves));
+        segs.swap(wm);
+    }
     if (nsegs > (uint32_t)(kConeWaves * 64)) throw std::runtime_error("schedule: unit fill exceeds the DMA segment table");
     const size_t lds_words = kBlobHeader + entries + nb + slot_area.size();
     const size_t runoff = (lds_words + 3) & ~(size_t)3;
@@ -745,8 +755,9 @@ static void validate_blob(const ConeItem& it, uint32_t p, int smax, int rw, cons
         throw std::runtime_error("schedule: malformed unit blob header");
     if (4 * fill > (uint32_t)kLdsBufFloats) throw std::runtime_error("schedule: unit fill exceeds the LDS level buffer");
     uint32_t c = 0;
+    const uint32_t K = (nseg + kConeWaves - 1) / kConeWaves;   // wave-major segment order
     for (uint32_t i = 0; i < nseg; ++i) {
-        const uint32_t* g = w + runoff + 4 * i;
+        const uint32_t* g = w + runoff + 4 * ((i % kConeWaves) * K + i / kConeWaves);
         if (g[0] != c || g[1] == 0 || g[1] > 64) throw std::runtime_error("schedule: DMA segments do not tile the fill");
         c += g[1];
     }
