@@ -193,6 +193,7 @@ constexpr uint64_t kTimelineCap = 1u << 21;
 enum : uint32_t {
     kConeStoreFromRegs = 1u,   // non-final passes store the output level straight from registers
     kConeFuse2 = 2u,           // two merge levels per LDS round trip where no level holds size-1 nodes
+    kConeSnrStride = 4u,       // final passes keep their output rows at a bank-friendly stride for the S/N
     kConeDiagNoSnr = 1u << 30, // diagnostics only (wrong results): skip the S/N epilogue
     kConeDiagNoMerge = 1u << 29, // diagnostics only (wrong results): skip the merge levels
     kConeDiagNoWrite = 1u << 28, // diagnostics only (wrong results): skip the level write-back
@@ -201,7 +202,7 @@ enum : uint32_t {
     kConeDiagNoDesc = 1u << 25,  // diagnostics only (wrong results): no descriptor table
     kConeDiagExitWait = 1u << 24, // A/B only: wait for the unit's stores before the workgroup ends
     kConeDiagNoFill = 1u << 23,  // diagnostics only (wrong results): metadata DMA only, no bottom-level fill
-    kConeDefaultFeatures = 3u
+    kConeDefaultFeatures = 3u   // kConeSnrStride measured neutral (8.55-8.60 vs 8.52-8.58 ms per cfg2 trial), off
 };
 enum : uint8_t { kSelLeaves = 0, kSelPing = 1, kSelPong = 2, kSelSnr = 3 };
 

@@ -877,7 +877,7 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
 // slot's rows A and B.
 template <int SMAX, int RW>
 __device__ __forceinline__ void write_rows_slots(float* base, float* dummy, const float (&v)[RW][SMAX], int p,
-                                                 int lane, uint32_t sw, int nq)
+                                                 int lane, uint32_t sw, int nq, int q)
 {
 #if RT_SLOT_OPAQUE_LANE
     asm volatile("" : "+v"(lane));
@@ -889,7 +889,7 @@ __device__ __forceinline__ void write_rows_slots(float* base, float* dummy, cons
             const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)sw, i / 2);
             if (i % 2 == 0 || (w >> 20) != kSlotOne) {
                 const int row = (int)((i % 2 == 0 ? w : w >> 10) & 1023u);
-                float* orow = base + row * p + lane;
+                float* orow = base + row * q + lane;
 #pragma unroll
                 for (int k = 0; k < SMAX; ++k) {
                     if (k < SMAX - 1) orow[64 * k] = v[i][k];
@@ -1048,7 +1048,8 @@ __device__ __forceinline__ void store_rows_lanes(const float (&v)[RW][1], int p,
 // the staging registers straight to global memory instead of back into LDS.
 template <int SMAX, int RW>
 __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int p, int L, int tid, bool st,
-                                             __amdgpu_buffer_rsrc_t rs, uint32_t st_o0, uint32_t flags, float* dummy)
+                                             __amdgpu_buffer_rsrc_t rs, uint32_t st_o0, uint32_t flags, float* dummy,
+                                             int qout)
 {
     const int lane = tid & 63, wave = tid >> 6;
     const bool tile = C.tile;
@@ -1115,7 +1116,9 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
                     return;
                 }
                 if (!(flags & kConeDiagNoBarrier)) lds_barrier();
-                if (!(flags & kConeDiagNoWrite)) write_rows_slots<SMAX, RW>(base, dummy, v, p, lane, sw, nq);
+                // the output level of a final pass at row stride qout (the S/N's)
+                if (!(flags & kConeDiagNoWrite))
+                    write_rows_slots<SMAX, RW>(base, dummy, v, p, lane, sw, nq, lo == 0 ? qout : p);
                 if (!(flags & kConeDiagNoBarrier)) lds_barrier();
             }
             return;
@@ -1730,10 +1733,22 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
             const float* dst = (U.dst == kSelPing ? a.ping : a.pong) + (uint64_t)U.trial * a.buf_stride + U.buf_off;
             const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(dst, (((uint32_t)U.m * (uint32_t)p + 3u) & ~3u) * 4u);
             const uint32_t o0 = (uint32_t)(U.node_start + U.s0) * (uint32_t)p * 4u;
-            if (L > 0 && !(a.flags & kConeDiagNoMerge))
-                merge_levels<SMAX, RW>(C, buf, p, L, tid, st_regs, rs, o0, a.flags, buf + kLdsBufFloats + 4 + (tid & 63));
-            RT_MARK(3);
             const int n0 = rows_at(C, 0);
+            // a final pass's output level at a row stride = 16 (mod 32): the
+            // S/N epilogue's lane groups (two rows of 16 lanes per 32-lane LDS
+            // group, odd chunk strides) then read and write on distinct banks
+            // (at stride p they collided on up to 10 of 32 banks)
+            int qout = p;
+            if constexpr (SMAX <= 5 && SMAX != kPack2) {
+                const int qp = p + ((48 - (p & 31)) & 31);
+                if (!st && L > 0 && C.slots && (a.flags & kConeFuse2) && (a.flags & kConeSnrStride) &&
+                    n0 * qp <= kLdsDataFloats)
+                    qout = qp;
+            }
+            if (L > 0 && !(a.flags & kConeDiagNoMerge))
+                merge_levels<SMAX, RW>(C, buf, p, L, tid, st_regs, rs, o0, a.flags, buf + kLdsBufFloats + 4 + (tid & 63),
+                                       qout);
+            RT_MARK(3);
             // the output level: dense rows from the buffer start, or (no merge
             // level) the single bottom row where the DMA left it
             float* const obase = L > 0 ? buf : buf + (C.table ? uni(bottom_offsets(C)[0]) : C.al);
@@ -1746,9 +1761,9 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
                 }
             } else {
 #ifdef RT_STAMPS
-                if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX>(a, U, obase, p, wl, n0, tid, whb, tl);
+                if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX>(a, U, obase, qout, wl, n0, tid, whb, tl);
 #else
-                if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX>(a, U, obase, p, wl, n0, tid, whb, nullptr);
+                if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX>(a, U, obase, qout, wl, n0, tid, whb, nullptr);
 #endif
             }
         }
