@@ -1374,6 +1374,45 @@ __device__ __forceinline__ void window_dispatch2(int w, const float (&z0)[CH + k
 #define RT_SNR_MARK(i) do { } while (0)
 #endif
 
+// Per-width constants of the S/N formula (snr.hpp:37-65): h + b and b of
+// width w over p bins.
+__device__ __forceinline__ void snr_width_consts(int w, int p, float* out)
+{
+    const float h = sqrtf((float)(p - w) / (float)(p * w));
+    const float b = (float)w / (float)(p - w) * h;
+    out[0] = h + b;
+    out[1] = b;
+}
+
+// Transposed S/N emit for row groups of G <= 16 lanes (A/B knob; 0: the
+// formula and a store per width in every lane)
+#ifndef RT_SNR_TEMIT
+#define RT_SNR_TEMIT 1
+#endif
+constexpr bool kSnrTransEmit = RT_SNR_TEMIT != 0;
+
+// max over each G-lane group (G = 8 or 16, groups aligned), in every lane
+// of the group: quad swaps, then the half-row and row mirrors (fmaxf never
+// returns a NaN operand over a number, as diff_max's comparison)
+template <int G>
+__device__ __forceinline__ float grp_allmax(float v)
+{
+    static_assert(G == 8 || G == 16, "DPP row groups");
+    v = fmaxf(v, dpp_f<0xB1>(v));     // quad_perm [1, 0, 3, 2]
+    v = fmaxf(v, dpp_f<0x4E>(v));     // quad_perm [2, 3, 0, 1]
+    v = fmaxf(v, dpp_f<0x141>(v));    // row_half_mirror: lane i <-> 7 - i
+    if constexpr (G == 16) v = fmaxf(v, dpp_f<0x140>(v));   // row_mirror: lane i <-> 15 - i
+    return v;
+}
+
+// Row passes without workgroup barriers (A/B knob: a row's lanes are one
+// wave, so the barrier per pass between the prefix writes and the window
+// reads is not needed for correctness; measured 9.10 vs 9.01 ms per cfg2
+// trial without it -- the waves' passes in lock step are faster -- so off).
+#ifndef RT_SNR_WAVE_LOCAL
+#define RT_SNR_WAVE_LOCAL 0
+#endif
+
 // NR rows per lane and pass (NR = 2: the lane's rows r and r + 512/G are
 // independent chains interleaved in one instruction stream, and half as many
 // row passes -- barriers, DPP scans -- per unit).
@@ -1425,7 +1464,13 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
 #pragma unroll
         for (int i = 0; i < CH; ++i)
 #pragma unroll
-            for (int k = 0; k < NR; ++k) part[k] = part[k] + (double)cp[k][i];
+            for (int k = 0; k < NR; ++k) {
+#ifdef RT_DIAG_SNR_F32
+                part[k] = (float)part[k] + cp[k][i];   // diagnostics only (wrong results)
+#else
+                part[k] = part[k] + (double)cp[k][i];
+#endif
+            }
         double acc[NR];
 #pragma unroll
         for (int k = 0; k < NR; ++k) {
@@ -1437,7 +1482,11 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
         for (int i = 0; i < CH; ++i)
 #pragma unroll
             for (int k = 0; k < NR; ++k) {
+#ifdef RT_DIAG_SNR_F32
+                acc[k] = (float)acc[k] + cp[k][i];   // diagnostics only (wrong results)
+#else
                 acc[k] = acc[k] + (double)cp[k][i];
+#endif
                 cp[k][i] = (float)acc[k];
             }
         float sum[NR];
@@ -1457,7 +1506,15 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
 #pragma unroll
             for (int i = 0; i < CH; ++i) cp[k][i] = i < cnt ? cp[k][i] : INFINITY;
         RT_SNR_MARK(7);
+#if RT_SNR_WAVE_LOCAL
+        // a row's G <= 64 lanes are one wave, and a wave's LDS accesses
+        // complete in order: its prefix writes are seen by its window reads
+        // below without a workgroup barrier (a compiler barrier only), so
+        // the waves of a unit run their row passes independently
+        __asm__ __volatile__("" ::: "memory");
+#else
         lds_barrier();                        // prefix rows visible to all lanes
+#endif
         RT_SNR_MARK(8);
         const float* crow[NR];
         uint32_t so[NR];
@@ -1468,15 +1525,33 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
             // range, which drops them (no exec-mask save/restore)
             so[k] = (active[k] && g == writer) ? (uint32_t)r[k] * nw * 4u : 0x80000000u;
         }
+        // transposed emit (G <= 16): the row's max of width iw goes to every
+        // lane of its group (DPP all-reduce) and lane g keeps widths g,
+        // g + G, ...; one S/N formula (one fp32 division) and one store per
+        // lane and slot after the widths, the stores of a row consecutive,
+        // instead of the formula and a store per width in every lane
+        constexpr bool TE = kSnrTransEmit && G <= 16;
+        constexpr int NSEL = TE ? kMaxWidths / G : 1;
+        float sel[NR][NSEL] = {};
         auto emit = [&](uint32_t iw, const float (&dmax)[NR]) {
-            // h + b and b of this width (per unit, in LDS: uniform reads)
-            const float hpb = __int_as_float(uni(__float_as_int(whb[2 * iw])));
-            const float b = __int_as_float(uni(__float_as_int(whb[2 * iw + 1])));
+            if constexpr (TE) {
 #pragma unroll
-            for (int k = 0; k < NR; ++k) {
-                const float dm = seg_max_dpp<G>(dmax[k], lane);
-                const float v = (hpb * dm - b * sum[k]) / U.stdnoise;
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srs, (int)(so[k] + iw * 4u), 0, 0);
+                for (int k = 0; k < NR; ++k) {
+                    const float dm = grp_allmax<G>(dmax[k]);
+#pragma unroll
+                    for (int sl = 0; sl < NSEL; ++sl)
+                        if (sl * G < (int)nw) sel[k][sl] = (int)iw == g + sl * G ? dm : sel[k][sl];
+                }
+            } else {
+                // h + b and b of this width (per unit, in LDS: uniform reads)
+                const float hpb = __int_as_float(uni(__float_as_int(whb[2 * iw])));
+                const float b = __int_as_float(uni(__float_as_int(whb[2 * iw + 1])));
+#pragma unroll
+                for (int k = 0; k < NR; ++k) {
+                    const float dm = seg_max_dpp<G>(dmax[k], lane);
+                    const float v = (hpb * dm - b * sum[k]) / U.stdnoise;
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srs, (int)(so[k] + iw * 4u), 0, 0);
+                }
             }
         };
         if constexpr (CH <= kSnrMaxChunk) {
@@ -1484,19 +1559,33 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
             float z[NR][CH + kSnrWin];
 #pragma unroll
             for (int k = 0; k < NR; ++k) {
-                // two opaque bases (row and row - p), slot offsets immediate
+                // two opaque bases (row and row - p), slot offsets immediate;
+                // one volatile read per element from the selected base (a
+                // plain read of each base was sunk into a branch per element,
+                // each with its own s_waitcnt lgkmcnt(0): 29 serialised LDS
+                // round trips per row pass)
                 lds_cptr za = (lds_cptr)(crow[k] + j0);
                 lds_cptr zb = za - p;
                 asm("" : "+v"(za), "+v"(zb));
+                // the wrap term as an addend (+0.0 before the wrap point: the
+                // prefix values are never -0.0, so x + 0.0 == x exactly), so
+                // no compare mask lives across the reads
+                float x[CH + kSnrWin], ad[CH + kSnrWin];
 #pragma unroll
                 for (int t = 0; t < CH + kSnrWin; ++t) {
                     const bool wrap = j0 + t >= p;
-                    const float va = za[t], vb = zb[t];
-                    z[k][t] = wrap ? __fadd_rn(vb, sum[k]) : va;
+                    ad[t] = wrap ? sum[k] : 0.0f;
+                    x[t] = lds_ld((wrap ? zb : za) + t);
                 }
+#pragma unroll
+                for (int t = 0; t < CH + kSnrWin; ++t) z[k][t] = __fadd_rn(x[t], ad[t]);
             }
             RT_SNR_MARK(9);
+#ifdef RT_DIAG_SNR_WIDTHS
+            for (uint32_t iw = 0; iw < min(nw, (uint32_t)RT_DIAG_SNR_WIDTHS); ++iw) {   // diagnostics only (wrong results)
+#else
             for (uint32_t iw = 0; iw < nw; ++iw) {
+#endif
                 const int w = uni(wl[iw]);
                 if (w <= kSnrWin) {
                     float dm[NR];
@@ -1535,6 +1624,23 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
             }
             emit(iw, dmax);
         }
+        if constexpr (TE) {
+#pragma unroll
+            for (int sl = 0; sl < NSEL; ++sl) {
+                if (sl * G < (int)nw) {
+                    const int iw = g + sl * G;
+                    const int iwc = min(iw, (int)nw - 1);
+                    const float hpb = whb[2 * iwc], b = whb[2 * iwc + 1];
+#pragma unroll
+                    for (int k = 0; k < NR; ++k) {
+                        const float v = (hpb * sel[k][sl] - b * sum[k]) / U.stdnoise;
+                        const uint32_t o = (active[k] && iw < (int)nw) ? ((uint32_t)r[k] * nw + (uint32_t)iw) * 4u
+                                                                       : 0x80000000u;
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srs, (int)o, 0, 0);
+                    }
+                }
+            }
+        }
         RT_SNR_MARK(10);
     }
 }
@@ -1563,15 +1669,11 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
     const int p = U.p;
     const int nev = (int)min((int64_t)nrows, (int64_t)U.rows_eval - (int64_t)U.s0);
     if (nev <= 0) return;
+#if !RT_SNR_WAVE_LOCAL
     // per-width constants of the S/N formula (snr.hpp:37-65), once per unit;
     // visible to every wave after the first barrier of the row passes
-    if (tid < (int)a.num_widths) {
-        const int w = wl[tid];
-        const float h = sqrtf((float)(p - w) / (float)(p * w));
-        const float b = (float)w / (float)(p - w) * h;
-        whb[2 * tid] = h + b;
-        whb[2 * tid + 1] = b;
-    }
+    if (tid < (int)a.num_widths) snr_width_consts(wl[tid], p, whb + 2 * tid);
+#endif
     // G lanes per row: the smallest power of two >= 8 whose chunks fit
     // kSnrMaxChunk columns; chunk lengths odd (the G chunks of a row start
     // on distinct banks)
@@ -1709,6 +1811,11 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
         const int p = U.p;
         const int L = U.levels;
         float* const buf = data[b];
+#if RT_SNR_WAVE_LOCAL
+        // a final pass's per-width S/N constants, published by the barrier
+        // below (the S/N row passes have no barrier of their own)
+        if (U.dst == kSelSnr && tid < (int)a.num_widths) snr_width_consts(wl[tid], p, whb + 2 * tid);
+#endif
         // every wave waits for its own DMA (the previous unit's stores count
         // in the same in-order counter), the barrier publishes all of them
         __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)
