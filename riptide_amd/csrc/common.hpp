@@ -202,7 +202,7 @@ enum : uint32_t {
     kConeDiagNoDesc = 1u << 25,  // diagnostics only (wrong results): no descriptor table
     kConeDiagExitWait = 1u << 24, // A/B only: wait for the unit's stores before the workgroup ends
     kConeDiagNoFill = 1u << 23,  // diagnostics only (wrong results): metadata DMA only, no bottom-level fill
-    kConeDefaultFeatures = 3u   // kConeSnrStride measured neutral (8.55-8.60 vs 8.52-8.58 ms per cfg2 trial), off
+    kConeDefaultFeatures = 7u   // kConeSnrStride: final-pass rows at a stride with room for the S/N wrap extension
 };
 enum : uint8_t { kSelLeaves = 0, kSelPing = 1, kSelPong = 2, kSelSnr = 3 };
 

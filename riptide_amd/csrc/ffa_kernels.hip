@@ -1426,6 +1426,9 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
     int j0 = min(g * c, p);
     int cnt = min(j0 + c, p) - j0;                // columns of this lane (may be 0)
     const int owner = (p - 1) / c;
+    // rows with room for the wrapped prefix extension (final-pass output
+    // levels at the S/N stride); only the register-window path uses it
+    const bool ext = CH <= kSnrMaxChunk && q >= p + kSnrWin;
     constexpr int kRowsPerSet = kConeBlock / G;
     constexpr int rows_per_pass = NR * kRowsPerSet;
     constexpr int writer = G - 1;
@@ -1501,6 +1504,21 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
 #pragma unroll
                 for (int i = 0; i < CH; ++i) *((active[k] && i < cnt) ? row[k] + i : dummy) = cp[k][i];
         }
+        // rows at a stride q >= p + kSnrWin: the wrapped prefix c[p + j] =
+        // c[j] + sum (kernels.hpp:88-97, j < kSnrWin) stored after the row by
+        // its own lanes (the wave's LDS accesses complete in order), so the
+        // window reads below take c[j0 .. j0 + CH + kSnrWin) without a wrap
+        if (ext) {
+#pragma unroll
+            for (int k = 0; k < NR; ++k) {
+                float* const rb = data + min(r[k], nev - 1) * q;
+#pragma unroll
+                for (int e0 = 0; e0 < kSnrWin; e0 += G) {
+                    const int e = e0 + g;
+                    if (active[k] && e < kSnrWin) rb[p + e] = __fadd_rn(lds_ld((lds_cptr)(rb + e)), sum[k]);
+                }
+            }
+        }
 #pragma unroll
         for (int k = 0; k < NR; ++k)
 #pragma unroll
@@ -1567,18 +1585,25 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
                 lds_cptr za = (lds_cptr)(crow[k] + j0);
                 lds_cptr zb = za - p;
                 asm("" : "+v"(za), "+v"(zb));
-                // the wrap term as an addend (+0.0 before the wrap point: the
-                // prefix values are never -0.0, so x + 0.0 == x exactly), so
-                // no compare mask lives across the reads
-                float x[CH + kSnrWin], ad[CH + kSnrWin];
+                if (ext) {
+                    // past the row: its wrapped extension (or, past that,
+                    // words only differences with masked columns read)
 #pragma unroll
-                for (int t = 0; t < CH + kSnrWin; ++t) {
-                    const bool wrap = j0 + t >= p;
-                    ad[t] = wrap ? sum[k] : 0.0f;
-                    x[t] = lds_ld((wrap ? zb : za) + t);
+                    for (int t = 0; t < CH + kSnrWin; ++t) z[k][t] = lds_ld(za + t);
+                } else {
+                    // the wrap term as an addend (+0.0 before the wrap point:
+                    // the prefix values are never -0.0, so x + 0.0 == x
+                    // exactly), so no compare mask lives across the reads
+                    float x[CH + kSnrWin], ad[CH + kSnrWin];
+#pragma unroll
+                    for (int t = 0; t < CH + kSnrWin; ++t) {
+                        const bool wrap = j0 + t >= p;
+                        ad[t] = wrap ? sum[k] : 0.0f;
+                        x[t] = lds_ld((wrap ? zb : za) + t);
+                    }
+#pragma unroll
+                    for (int t = 0; t < CH + kSnrWin; ++t) z[k][t] = __fadd_rn(x[t], ad[t]);
                 }
-#pragma unroll
-                for (int t = 0; t < CH + kSnrWin; ++t) z[k][t] = __fadd_rn(x[t], ad[t]);
             }
             RT_SNR_MARK(9);
 #ifdef RT_DIAG_SNR_WIDTHS
@@ -1847,7 +1872,9 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
             // (at stride p they collided on up to 10 of 32 banks)
             int qout = p;
             if constexpr (SMAX <= 5 && SMAX != kPack2) {
-                const int qp = p + ((48 - (p & 31)) & 31);
+                // >= p + kSnrWin (the S/N's wrapped prefix extension) and
+                // = 16 (mod 32)
+                const int qp = p + kSnrWin + ((16 - ((p + kSnrWin) & 31)) & 31);
                 if (!st && L > 0 && C.slots && (a.flags & kConeFuse2) && (a.flags & kConeSnrStride) &&
                     n0 * qp <= kLdsDataFloats)
                     qout = qp;
