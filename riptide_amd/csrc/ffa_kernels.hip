@@ -1429,6 +1429,8 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
     // rows with room for the wrapped prefix extension (final-pass output
     // levels at the S/N stride); only the register-window path uses it
     const bool ext = CH <= kSnrMaxChunk && q >= p + kSnrWin;
+    // rows with room past p for a lane's whole CH-column prefix write
+    const bool wfull = q >= p + CH;
     constexpr int kRowsPerSet = kConeBlock / G;
     constexpr int rows_per_pass = NR * kRowsPerSet;
     constexpr int writer = G - 1;
@@ -1459,6 +1461,9 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
             for (int i = 0; i < CH; ++i) {
                 const float x = row[k][i];
                 cp[k][i] = i < cnt ? x : 0.0f;
+                // the select on the float, before the fp64 conversion (else
+                // two selects on the converted halves)
+                asm("" : "+v"(cp[k][i]));
             }
         // fp64 prefix: the masked columns add +0.0 (the partial sums start at
         // +0.0 and are never -0.0, so the additions are exact no-ops)
@@ -1496,13 +1501,41 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
 #pragma unroll
         for (int k = 0; k < NR; ++k) sum[k] = __shfl((float)acc[k], owner, G);
         {
-            // columns past the lane's chunk (and rows past nev) go to a dummy
-            // word in the LDS pad: an address select instead of exec masks
-            float* const dummy = data + kLdsDataFloats + 4 + lane;
+            // columns past the lane's chunk (and rows past nev) go to dummy
+            // words in the LDS pad: a base select per column (the column an
+            // immediate offset) instead of exec masks
+            typedef __attribute__((address_space(3))) float* lds_ptr;
+            if (wfull) {
+                // every lane of an active row writes all CH columns, last
+                // column first: a column past the lane's chunk is the next
+                // lane's column i - c, which that lane writes later (a
+                // wave's LDS writes land in order), or lies past the row
+                // inside its stride (q >= p + CH)
 #pragma unroll
-            for (int k = 0; k < NR; ++k)
+                for (int k = 0; k < NR; ++k) {
+                    if (active[k]) {
+                        // volatile: the compiler keeps the descending order
+                        volatile __attribute__((address_space(3))) float* const rk =
+                            (volatile __attribute__((address_space(3))) float*)row[k];
 #pragma unroll
-                for (int i = 0; i < CH; ++i) *((active[k] && i < cnt) ? row[k] + i : dummy) = cp[k][i];
+                        for (int i = CH - 1; i >= 0; --i) rk[i] = cp[k][i];
+                    }
+                }
+            } else {
+                const lds_ptr dummy = (lds_ptr)(data + kLdsDataFloats + 4);
+#pragma unroll
+                for (int k = 0; k < NR; ++k) {
+                    int cw = active[k] ? cnt : 0;
+                    asm("" : "+v"(cw));
+                    const lds_ptr rk = (lds_ptr)row[k];
+#pragma unroll
+                    for (int i = 0; i < CH; ++i) {
+                        lds_ptr b = i < cw ? rk : dummy;
+                        asm("" : "+v"(b));
+                        b[i] = cp[k][i];
+                    }
+                }
+            }
         }
         // rows at a stride q >= p + kSnrWin: the wrapped prefix c[p + j] =
         // c[j] + sum (kernels.hpp:88-97, j < kSnrWin) stored after the row by
@@ -1515,7 +1548,9 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
 #pragma unroll
                 for (int e0 = 0; e0 < kSnrWin; e0 += G) {
                     const int e = e0 + g;
-                    if (active[k] && e < kSnrWin) rb[p + e] = __fadd_rn(lds_ld((lds_cptr)(rb + e)), sum[k]);
+                    if (active[k] && e < kSnrWin)
+                        *(volatile __attribute__((address_space(3))) float*)(rb + p + e) =
+                            __fadd_rn(lds_ld((lds_cptr)(rb + e)), sum[k]);
                 }
             }
         }
@@ -1872,12 +1907,13 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
             // (at stride p they collided on up to 10 of 32 banks)
             int qout = p;
             if constexpr (SMAX <= 5 && SMAX != kPack2) {
-                // >= p + kSnrWin (the S/N's wrapped prefix extension) and
-                // = 16 (mod 32)
-                const int qp = p + kSnrWin + ((16 - ((p + kSnrWin) & 31)) & 31);
-                if (!st && L > 0 && C.slots && (a.flags & kConeFuse2) && (a.flags & kConeSnrStride) &&
-                    n0 * qp <= kLdsDataFloats)
-                    qout = qp;
+                // = 16 (mod 32) and >= p + kSnrMaxChunk (room for the S/N's
+                // whole-chunk prefix writes and its wrapped prefix
+                // extension), else >= p + kSnrWin (the extension only)
+                const int qa = p + kSnrMaxChunk + ((16 - ((p + kSnrMaxChunk) & 31)) & 31);
+                const int qb = p + kSnrWin + ((16 - ((p + kSnrWin) & 31)) & 31);
+                if (!st && L > 0 && C.slots && (a.flags & kConeFuse2) && (a.flags & kConeSnrStride))
+                    qout = n0 * qa <= kLdsDataFloats ? qa : (n0 * qb <= kLdsDataFloats ? qb : p);
             }
             if (L > 0 && !(a.flags & kConeDiagNoMerge))
                 merge_levels<SMAX, RW>(C, buf, p, L, tid, st_regs, rs, o0, a.flags, buf + kLdsBufFloats + 4 + (tid & 63),
