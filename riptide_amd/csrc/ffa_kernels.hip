@@ -1298,9 +1298,25 @@ __device__ __forceinline__ float window_max(const float (&z)[CH + kSnrWin], cons
     }
     return d[0];
 #else
+    // v_sub_f32 / v_max3_f32 as volatile asm: the width's work stays inside
+    // its switch case (from plain code the compiler evaluated every case --
+    // all kSnrWin widths -- ahead of the width loop in every row pass).
+    // v_max3_f32 (IEEE mode) never returns a quiet-NaN operand over a
+    // number, as diff_max's comparison (kernels.hpp:50-60).
     float dm = -INFINITY;
 #pragma unroll
-    for (int i = 0; i < CH; ++i) dm = fmaxf(dm, __fsub_rn(z[i + W], cp[i]));
+    for (int i = 0; i + 1 < CH; i += 2) {
+        float t0, t1;
+        asm volatile("v_sub_f32 %1, %3, %4\n\tv_sub_f32 %2, %5, %6\n\tv_max3_f32 %0, %0, %1, %2"
+                     : "+v"(dm), "=&v"(t0), "=&v"(t1)
+                     : "v"(z[i + W]), "v"(cp[i]), "v"(z[i + 1 + W]), "v"(cp[i + 1]));
+    }
+    if constexpr (CH & 1) {
+        float t0;
+        asm volatile("v_sub_f32 %1, %2, %3\n\tv_max_f32 %0, %0, %1"
+                     : "+v"(dm), "=&v"(t0)
+                     : "v"(z[CH - 1 + W]), "v"(cp[CH - 1]));
+    }
     return dm;
 #endif
 }
@@ -1398,10 +1414,15 @@ template <int G>
 __device__ __forceinline__ float grp_allmax(float v)
 {
     static_assert(G == 8 || G == 16, "DPP row groups");
-    v = fmaxf(v, dpp_f<0xB1>(v));     // quad_perm [1, 0, 3, 2]
-    v = fmaxf(v, dpp_f<0x4E>(v));     // quad_perm [2, 3, 0, 1]
-    v = fmaxf(v, dpp_f<0x141>(v));    // row_half_mirror: lane i <-> 7 - i
-    if constexpr (G == 16) v = fmaxf(v, dpp_f<0x140>(v));   // row_mirror: lane i <-> 15 - i
+    // v_max_f32 with a DPP source (no canonicalising moves around a
+    // separate DPP move); s_nop 1: the DPP read of a VGPR written by the
+    // previous VALU instruction
+    asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                 "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+                 "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf"
+                 : "+v"(v));
+    if constexpr (G == 16)
+        asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf" : "+v"(v));
     return v;
 }
 
