@@ -1458,6 +1458,9 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
     const uint32_t nw = a.num_widths;
     float* snr = a.snr + (uint64_t)U.trial * a.snr_stride + (U.snr_row + (uint64_t)U.s0) * (uint64_t)nw;
     const __amdgpu_buffer_rsrc_t srs = buffer_rsrc(snr, (uint32_t)nev * nw * 4u);
+    // the widths in lanes (lane i: width i), taken per width by v_readlane
+    // instead of an LDS read and its wait
+    const int wlane = wl[min(lane, (int)nw - 1)];
     for (int base = 0; base < nev; base += rows_per_pass) {
         // opaque per row pass: the column masks (i < cnt, j0 + k >= p) are
         // recomputed by one v_cmp each instead of being hoisted out of the
@@ -1667,7 +1670,7 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
 #else
             for (uint32_t iw = 0; iw < nw; ++iw) {
 #endif
-                const int w = uni(wl[iw]);
+                const int w = __builtin_amdgcn_readlane(wlane, (int)iw);
                 if (w <= kSnrWin) {
                     float dm[NR];
 #pragma unroll
@@ -1683,7 +1686,7 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
         }
         // wider widths: the window c[j0 + w ..] read from LDS per width
         for (uint32_t iw = 0; iw < nw; ++iw) {
-            const int w = uni(wl[iw]);
+            const int w = __builtin_amdgcn_readlane(wlane, (int)iw);
             if (CH <= kSnrMaxChunk && w <= kSnrWin) continue;
             float dmax[NR];
             const int last = max(cnt - 1, 0);
