@@ -20,6 +20,9 @@ from .reading import _raw_samples
 
 log = logging.getLogger("riptide.worker_pool")
 
+# host threads reading a chunk's files
+_READ_THREADS = 8
+
 
 def iterate_chunks(fnames, chunksize=1):
     """DMIterator.iterate_filenames (pipeline/dmiter.py:231-243) over an
@@ -55,12 +58,18 @@ class GpuWorkerPool:
         return self.process_fname_list([fname])
 
     def process_fname_list(self, fnames):
-        raws, metas, tsamps = [], [], []
-        for fn in fnames:
-            raw, meta, tsamp = _raw_samples(fn, self.fmt)
-            raws.append(raw)
-            metas.append(meta)
-            tsamps.append(tsamp)
+        # the chunk's files are read concurrently (np.fromfile releases the
+        # GIL), as rffa's pool reads one file per process
+        fnames = list(fnames)
+        if len(fnames) > 1:
+            from concurrent.futures import ThreadPoolExecutor
+            with ThreadPoolExecutor(max_workers=min(len(fnames), _READ_THREADS)) as ex:
+                loaded = list(ex.map(lambda fn: _raw_samples(fn, self.fmt), fnames))
+        else:
+            loaded = [_raw_samples(fn, self.fmt) for fn in fnames]
+        raws = [t[0] for t in loaded]
+        metas = [t[1] for t in loaded]
+        tsamps = [t[2] for t in loaded]
         per_file = self.searcher.search_samples(raws, tsamps, metas)
         for meta, peaks in zip(metas, per_file):
             log.debug(f"Done searching DM = {meta.get('dm')}, peaks found: {len(peaks)}")
