@@ -958,12 +958,20 @@ __device__ __forceinline__ void merge_step_lanes(const UnitCtx& C, const float* 
 #define RT_LANES_GROUP 4
 #endif
     constexpr int G = RT_LANES_GROUP;
-    auto row = [&](int i) {
-        int r = 2 * (wave + kConeWaves * i) + h;
-        r = r < nrows ? r : nrows - 1;
+    auto rowidx = [&](int i) {
+        const int r = 2 * (wave + kConeWaves * i) + h;
+        return r < nrows ? r : nrows - 1;
+    };
+    // the next row's entry is read before this row's (volatile) data reads:
+    // LDS reads complete in order, so a descriptor read issued after them
+    // waited for all of them (lgkmcnt(0)) before its decode could start
+    uint2 enext = make_uint2(0u, 0u);
+    auto row = [&](int i, bool pre) {
+        const int r = rowidx(i);
         if constexpr (TWO) {
             // the host-resolved row: source rows q0..q3 of level lo + 2, rolls
-            const uint2 e = step[r];
+            const uint2 e = enext;
+            if (pre) enext = step[rowidx(i + 1)];
             const uint32_t q0 = e.x & 1023u, q1 = (e.x >> 10) & 1023u, q2 = (e.x >> 20) & 1023u, q3 = e.y & 1023u;
             const int sH = (int)((e.y >> 10) & 63u), sh = (int)((e.y >> 16) & 63u), sTT = (int)((e.y >> 22) & 63u);
             const int o0 = FIRST ? loff[q0] : (int)__umul24(q0, (uint32_t)p);
@@ -997,8 +1005,10 @@ __device__ __forceinline__ void merge_step_lanes(const UnitCtx& C, const float* 
 #pragma unroll
     for (int g = 0; g < RW; g += G) {
         if (2 * (wave + kConeWaves * g) < nrows) {
+            const int ge = g + G < RW ? g + G : RW;
+            if constexpr (TWO) enext = step[rowidx(g)];
 #pragma unroll
-            for (int i = g; i < (g + G < RW ? g + G : RW); ++i) row(i);
+            for (int i = g; i < ge; ++i) row(i, i + 1 < ge);
         }
     }
 }
