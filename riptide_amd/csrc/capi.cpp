@@ -1045,7 +1045,7 @@ int rt_segment_order_stats_device(const float* d_snrs, size_t batch, size_t snr_
         if (!batch || !num_widths || !nseg) return RT_OK;
         if (per_seg == 0 || nseg * per_seg > length) throw std::invalid_argument("segments exceed the periodogram");
         if (per_seg > (size_t)kMaxSegmentPoints)
-            throw std::invalid_argument("segment longer than the device sort (4096 points)");
+            throw std::invalid_argument("segment longer than the device sort (32768 points)");
         if (!nranks || nranks > (size_t)kMaxSegmentRanks) throw std::invalid_argument("1 to 8 ranks per segment");
         for (size_t r = 0; r < nranks; ++r)
             if (ranks[r] >= per_seg) throw std::invalid_argument("rank outside the segment");

@@ -49,7 +49,7 @@ hipError_t launch_ffa_level(const float* in, float* out, const uint2* d_nodes, u
                             uint32_t rows, uint32_t p, hipStream_t s);
 
 // peaks_kernels.hip
-constexpr int kMaxSegmentPoints = 4096;   // rows of one peak-detection segment sorted in LDS
+constexpr int kMaxSegmentPoints = 32768;  // rows of one peak-detection segment sorted in LDS (128 KiB)
 constexpr int kMaxSegmentRanks = 8;       // order statistics per segment (host ranks array)
 hipError_t launch_segment_order_stats(const float* snrs, uint64_t snr_stride, uint32_t batch, uint32_t W,
                                       uint32_t nseg, uint32_t per_seg, const uint32_t* ranks, uint32_t nranks,

@@ -28,30 +28,32 @@ struct SegRanks {           // ranks of the order statistics, passed by value
     uint32_t r[kMaxSegmentRanks];
 };
 
-__global__ __launch_bounds__(kPeakBlock) void segment_order_stats_kernel(
+// One block per (segment, width, trial); the segment padded to n2 (a power
+// of two) in dynamic LDS: 256 threads up to 4096 points, 1024 beyond (up to
+// kMaxSegmentPoints = 32768, 128 KiB).
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void segment_order_stats_kernel(
     const float* __restrict__ snrs, uint64_t snr_stride, uint32_t W, uint32_t per_seg, uint32_t n2,
     SegRanks ranks, uint32_t nranks, float* __restrict__ out)
 {
-    __shared__ float key[kMaxSegmentPoints];
-    __shared__ int has_nan;
+    extern __shared__ __attribute__((aligned(16))) float key[];
     const uint32_t seg = blockIdx.x, iw = blockIdx.y, trial = blockIdx.z;
     const uint32_t nseg = gridDim.x;
     const float* s = snrs + (uint64_t)trial * snr_stride + (uint64_t)seg * per_seg * W + iw;
-    if (threadIdx.x == 0) has_nan = 0;
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < n2; i += kPeakBlock) {
+    int nan_seen = 0;
+    for (uint32_t i = threadIdx.x; i < n2; i += BLOCK) {
         float v = INFINITY;
         if (i < per_seg) {
             v = s[(uint64_t)i * W];
-            if (v != v) has_nan = 1;
+            nan_seen |= v != v;
         }
         key[i] = v;
     }
-    __syncthreads();
+    const int has_nan = __syncthreads_or(nan_seen);
     // bitonic sort, ascending
     for (uint32_t k = 2; k <= n2; k <<= 1) {
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = threadIdx.x; i < n2; i += kPeakBlock) {
+            for (uint32_t i = threadIdx.x; i < n2; i += BLOCK) {
                 const uint32_t ixj = i ^ j;
                 if (ixj > i) {
                     const float a = key[i], b = key[ixj];
@@ -99,8 +101,22 @@ hipError_t launch_segment_order_stats(const float* snrs, uint64_t snr_stride, ui
     for (uint32_t i = 0; i < nranks; ++i) rk.r[i] = ranks[i];
     uint32_t n2 = 1;
     while (n2 < per_seg) n2 <<= 1;
-    hipLaunchKernelGGL(segment_order_stats_kernel, dim3(nseg, W, batch), dim3(kPeakBlock), 0, s, snrs, snr_stride, W,
-                       per_seg, n2, rk, nranks, out);
+    const size_t lds = (size_t)n2 * sizeof(float);
+    if (n2 <= 4096) {
+        hipLaunchKernelGGL(segment_order_stats_kernel<kPeakBlock>, dim3(nseg, W, batch), dim3(kPeakBlock), lds, s,
+                           snrs, snr_stride, W, per_seg, n2, rk, nranks, out);
+    } else {
+        static bool attr = false;    // > 64 KiB of dynamic LDS: opt in once
+        if (!attr) {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(segment_order_stats_kernel<1024>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)(kMaxSegmentPoints * sizeof(float)));
+            if (e != hipSuccess) return e;
+            attr = true;
+        }
+        hipLaunchKernelGGL(segment_order_stats_kernel<1024>, dim3(nseg, W, batch), dim3(1024), lds, s, snrs,
+                           snr_stride, W, per_seg, n2, rk, nranks, out);
+    }
     return hipGetLastError();
 }
 

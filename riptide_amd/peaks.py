@@ -88,7 +88,7 @@ class PeakFinder:
         self.nseg = ceil(abs(f[-1] - f[0]) / w) if L else 0
         self.per_seg = L // self.nseg if self.nseg else 0
         n = self.nseg * self.per_seg
-        self.device_ok = 0 < self.per_seg <= 4096
+        self.device_ok = 0 < self.per_seg <= 32768      # kMaxSegmentPoints (peaks_kernels.hip)
         if self.device_ok:
             self.fc = np.median(f[:n].reshape(self.nseg, self.per_seg), axis=1)
             self.logfc = np.log(self.fc)

@@ -352,6 +352,58 @@ def test_device_find_peaks_matches_host(rt):
     _device_vs_host_peaks(rt, plan, snr, tobs, minseg=10 ** 6)
 
 
+@pytest.mark.parametrize("per_seg", [4097, 10000, 32768])
+def test_segment_order_stats_long_segments(rt, per_seg):
+    """Segments longer than 4096 points (the 1024-thread, dynamic-LDS sort;
+    cfg5's short range has ~8K-point segments): the requested ranks of every
+    (trial, width, segment) equal numpy's sorted values, NaN segments NaN."""
+    import ctypes
+    import torch
+    from riptide_amd import _lib
+    L_ = _lib.load()
+    B, W, nseg = 2, 3, 3
+    L = nseg * per_seg + 5
+    rng = np.random.default_rng(per_seg)
+    snr = rng.standard_normal((B, L, W)).astype(np.float32)
+    snr[1, per_seg + 7, 2] = np.nan                     # trial 1, width 2, segment 1
+    ranks = np.array([0, per_seg // 4, per_seg // 2, per_seg - 1], dtype=np.uint32)
+    d = torch.from_numpy(snr).cuda()
+    out = torch.empty((B, W, nseg, ranks.size), dtype=torch.float32, device="cuda")
+    rc = L_.rt_segment_order_stats_device(_lib.ptr(d), B, L * W, L, W, nseg, per_seg, _lib.ptr(ranks), ranks.size,
+                                          _lib.ptr(out), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert rc == 0, L_.rt_last_error()
+    got = out.cpu().numpy()
+    for b in range(B):
+        for iw in range(W):
+            for sg in range(nseg):
+                col = snr[b, sg * per_seg:(sg + 1) * per_seg, iw]
+                if np.isnan(col).any():
+                    assert np.isnan(got[b, iw, sg]).all()
+                else:
+                    assert np.array_equal(got[b, iw, sg], np.sort(col)[ranks])
+
+
+def test_device_find_peaks_long_segments(rt):
+    """find_peaks with segments of more than 4096 periods on the device path
+    (a wide segwidth), identical to the host computation."""
+    import torch
+    from riptide_amd import engine
+    from riptide_amd.peaks import PeakFinder
+    case = inputs.PGRAM_CASES[1]
+    plan = engine.PeriodogramPlan.for_search(case["n"], case["tsamp"], case["pmin"], case["pmax"],
+                                             case["bmin"], case["bmax"], ducy_max=case["ducy_max"])
+    tobs = case["n"] * case["tsamp"]
+    periods, _ = plan.grid()
+    f = 1.0 / periods
+    # a segment width giving segments of ~5000 periods
+    segwidth = 5000.0 / plan.length * abs(f[-1] - f[0]) * tobs
+    assert 4096 < PeakFinder(plan, tobs, segwidth=segwidth).per_seg <= 32768
+    xs = np.stack([inputs.with_signal(case["n"], case["tsamp"], s, 0.41, 14.0) for s in range(2)])
+    d = engine.deredden_normalise(torch.from_numpy(xs).cuda(), 1001, 101)
+    snr = plan.run(d)
+    _device_vs_host_peaks(rt, plan, snr, tobs, segwidth=segwidth, minseg=2)
+
+
 @pytest.mark.parametrize("name", ["cfg1", "cfg2"])
 def test_device_find_peaks_full_config(rt, golden_full, name):
     import torch
