@@ -303,14 +303,26 @@ def read_presto(fname):
 # ---------------------------------------------------------------------------
 # Device batch loading
 # ---------------------------------------------------------------------------
-def _raw_samples(fname, fmt, extra_keys=None):
-    """(raw numpy samples as stored, Metadata, tsamp) without the float cast."""
+def _raw_samples(fname, fmt, extra_keys=None, staging=None):
+    """(raw numpy samples as stored, Metadata, tsamp) without the float cast.
+    `staging(nbytes)`, if given, returns a writable uint8 numpy array of at
+    least nbytes (page-locked host memory) that SIGPROC samples are read into
+    directly; the samples returned are then a view of it."""
     if fmt == "sigproc":
         sh = SigprocHeader(fname, extra_keys=extra_keys)
         meta = sigproc_metadata(sh)
+        dt = np.dtype(sigproc_sample_dtype(meta))
         with open(sh.fname, "rb") as f:
             f.seek(sh.bytesize)
-            raw = np.fromfile(f, dtype=sigproc_sample_dtype(meta))
+            if staging is None:
+                raw = np.fromfile(f, dtype=dt)
+            else:
+                nbytes = (os.path.getsize(sh.fname) - sh.bytesize) // dt.itemsize * dt.itemsize
+                buf = staging(nbytes)[:nbytes]
+                got = f.readinto(memoryview(buf))
+                if got != nbytes:
+                    raise OSError(f"short read from {sh.fname}: {got} of {nbytes} bytes")
+                raw = buf.view(dt)
         return raw, meta, sh["tsamp"]
     if fmt == "presto":
         data, meta, tsamp = read_presto(fname)
@@ -338,12 +350,15 @@ def upload_samples(raws, device=None, stream=None):
         out = torch.empty((len(raws), n), dtype=torch.float32, device=dev)
         for b, raw in enumerate(raws):
             raw = np.ascontiguousarray(raw)
+            # non_blocking: an asynchronous DMA when the samples sit in
+            # page-locked memory (_raw_samples' staging); the caller keeps
+            # that memory until the stream has consumed it
             if raw.dtype == np.float32:
-                out[b].copy_(torch.from_numpy(raw))
+                out[b].copy_(torch.from_numpy(raw), non_blocking=True)
                 continue
             if raw.dtype not in kinds:
                 raise ValueError(f"unsupported sample type {raw.dtype}")
-            staged = torch.from_numpy(raw.view(np.uint8)).to(dev)
+            staged = torch.from_numpy(raw.view(np.uint8)).to(dev, non_blocking=True)
             _lib.check(L.rt_convert_samples_device(_lib.ptr(staged), n, kinds[raw.dtype], _lib.ptr(out[b]),
                                                    _stream_handle(s)))
     return out

@@ -54,6 +54,23 @@ class GpuWorkerPool:
         self.batch = int(batch)
         self.searcher = EngineSearcher(self.deredden_params, self.range_confs, device=device, batch=self.batch)
 
+    def _stager(self, slot):
+        """staging(nbytes) for file slot `slot` of a chunk: a page-locked
+        uint8 buffer, grown when a file needs more (None without a GPU)."""
+        import torch
+        if not torch.cuda.is_available():
+            return None
+        if not hasattr(self, "_pinned"):
+            self._pinned = {}
+
+        def staging(nbytes):
+            buf = self._pinned.get(slot)
+            if buf is None or buf.numel() < nbytes:
+                buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, pin_memory=True)
+                self._pinned[slot] = buf
+            return buf.numpy()
+        return staging
+
     def process_fname(self, fname):
         return self.process_fname_list([fname])
 
@@ -61,12 +78,18 @@ class GpuWorkerPool:
         # the chunk's files are read concurrently (np.fromfile releases the
         # GIL), as rffa's pool reads one file per process
         fnames = list(fnames)
+        # SIGPROC samples land in page-locked slots reused across chunks (one
+        # per file of a chunk), so the uploads are asynchronous DMAs; every
+        # device use of a chunk's samples has completed when search_samples
+        # returns (its peak lists are on the host), before the slots are
+        # refilled by the next call
+        stagers = [self._stager(i) for i in range(len(fnames))] if self.fmt == "sigproc" else [None] * len(fnames)
         if len(fnames) > 1:
             from concurrent.futures import ThreadPoolExecutor
             with ThreadPoolExecutor(max_workers=min(len(fnames), _READ_THREADS)) as ex:
-                loaded = list(ex.map(lambda fn: _raw_samples(fn, self.fmt), fnames))
+                loaded = list(ex.map(lambda a: _raw_samples(a[0], self.fmt, staging=a[1]), zip(fnames, stagers)))
         else:
-            loaded = [_raw_samples(fn, self.fmt) for fn in fnames]
+            loaded = [_raw_samples(fn, self.fmt, staging=st) for fn, st in zip(fnames, stagers)]
         raws = [t[0] for t in loaded]
         metas = [t[1] for t in loaded]
         tsamps = [t[2] for t in loaded]
