@@ -1410,20 +1410,21 @@ __device__ __forceinline__ void snr_width_consts(int w, int p, float* out)
     out[1] = b;
 }
 
-// Transposed S/N emit for row groups of G <= 16 lanes (A/B knob; 0: the
-// formula and a store per width in every lane)
+// Transposed S/N emit (A/B knob; 0: the formula and a store per width in
+// every lane)
 #ifndef RT_SNR_TEMIT
 #define RT_SNR_TEMIT 1
 #endif
 constexpr bool kSnrTransEmit = RT_SNR_TEMIT != 0;
 
-// max over each G-lane group (G = 8 or 16, groups aligned), in every lane
-// of the group: quad swaps, then the half-row and row mirrors (fmaxf never
-// returns a NaN operand over a number, as diff_max's comparison)
+// max over each G-lane group (G = 8 .. 64, groups aligned), in every lane
+// of the group: quad swaps, then the half-row and row mirrors, then (G >= 32)
+// cross-row exchanges (max never returns a NaN operand over a number, as
+// diff_max's comparison)
 template <int G>
 __device__ __forceinline__ float grp_allmax(float v)
 {
-    static_assert(G == 8 || G == 16, "DPP row groups");
+    static_assert(G == 8 || G == 16 || G == 32 || G == 64, "lane groups");
     // v_max_f32 with a DPP source (no canonicalising moves around a
     // separate DPP move); s_nop 1: the DPP read of a VGPR written by the
     // previous VALU instruction
@@ -1431,8 +1432,12 @@ __device__ __forceinline__ float grp_allmax(float v)
                  "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
                  "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf"
                  : "+v"(v));
-    if constexpr (G == 16)
+    if constexpr (G >= 16)
         asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf" : "+v"(v));
+    // 32- and 64-lane groups: lane i <-> i ^ 16 by ds_swizzle (xor mask 16
+    // inside 32 lanes), lane i <-> i ^ 32 by ds_bpermute
+    if constexpr (G >= 32) v = fmaxf(v, __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x401F)));
+    if constexpr (G == 64) v = fmaxf(v, __shfl_xor(v, 32, 64));
     return v;
 }
 
@@ -1612,13 +1617,13 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
             // range, which drops them (no exec-mask save/restore)
             so[k] = (active[k] && g == writer) ? (uint32_t)r[k] * nw * 4u : 0x80000000u;
         }
-        // transposed emit (G <= 16): the row's max of width iw goes to every
+        // transposed emit: the row's max of width iw goes to every
         // lane of its group (DPP all-reduce) and lane g keeps widths g,
         // g + G, ...; one S/N formula (one fp32 division) and one store per
         // lane and slot after the widths, the stores of a row consecutive,
         // instead of the formula and a store per width in every lane
-        constexpr bool TE = kSnrTransEmit && G <= 16;
-        constexpr int NSEL = TE ? kMaxWidths / G : 1;
+        constexpr bool TE = kSnrTransEmit;
+        constexpr int NSEL = TE ? (kMaxWidths + G - 1) / G : 1;
         float sel[NR][NSEL] = {};
         auto emit = [&](uint32_t iw, const float (&dmax)[NR]) {
             if constexpr (TE) {
