@@ -38,6 +38,38 @@ def test_sigproc_round_trip(tmp_path, nbits, signed, dtype):
     assert np.isclose(sh.skycoord.dec_deg, -(30 + 12 / 60 + 34.5 / 3600))
 
 
+@pytest.mark.parametrize("nbits,signed,dtype", [(32, None, np.float32), (8, True, np.int8), (8, False, np.uint8)])
+def test_raw_samples_into_staging(tmp_path, nbits, signed, dtype):
+    """_raw_samples reading straight into a caller's staging buffer (the
+    worker pool's page-locked slots): the same samples as np.fromfile, a view
+    of that buffer, and a slot larger than the file is fine."""
+    from riptide_amd.reading import _raw_samples
+    rng = np.random.RandomState(7 + nbits)
+    if dtype == np.float32:
+        data = rng.normal(size=777).astype(np.float32)
+    else:
+        info = np.iinfo(dtype)
+        data = rng.randint(info.min, info.max + 1, size=779).astype(dtype)
+    hdr = dict(HDR, nbits=nbits)
+    if signed is not None:
+        hdr["signed"] = signed
+    fn = str(tmp_path / "s.tim")
+    write_sigproc(fn, data, hdr)
+    slot = np.zeros(4 * 1024, dtype=np.uint8)
+    asked = []
+
+    def staging(nbytes):
+        asked.append(nbytes)
+        return slot
+
+    raw, meta, tsamp = _raw_samples(fn, "sigproc", staging=staging)
+    ref, _, _ = _raw_samples(fn, "sigproc")
+    assert asked == [data.nbytes]
+    assert raw.dtype == ref.dtype == dtype and np.array_equal(raw, ref) and np.array_equal(raw, data)
+    assert np.shares_memory(raw, slot)
+    assert tsamp == HDR["tsamp"] and meta["dm"] == HDR["refdm"]
+
+
 def test_sigproc_errors(tmp_path):
     fn = str(tmp_path / "bad.tim")
     write_sigproc(fn, np.zeros(10, np.float32), dict(HDR, nchans=4))
