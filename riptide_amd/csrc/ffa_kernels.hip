@@ -1441,12 +1441,13 @@ __device__ __forceinline__ float grp_allmax(float v)
     return v;
 }
 
-// Row passes without workgroup barriers (A/B knob: a row's lanes are one
-// wave, so the barrier per pass between the prefix writes and the window
-// reads is not needed for correctness; measured 9.10 vs 9.01 ms per cfg2
-// trial without it -- the waves' passes in lock step are faster -- so off).
+// Row passes without workgroup barriers: a row's lanes are one wave, so the
+// barrier per pass between the prefix writes and the window reads is not
+// needed for correctness.  A/B (ms per trial): on the round-2 mid S/N 9.10
+// vs 9.01 (slower); on the final S/N (transposed emit, no wrap selects)
+// cfg2 8.36 vs 8.43, cfg4 1.327 vs 1.34 -- on.
 #ifndef RT_SNR_WAVE_LOCAL
-#define RT_SNR_WAVE_LOCAL 0
+#define RT_SNR_WAVE_LOCAL 1
 #endif
 
 // NR rows per lane and pass (NR = 2: the lane's rows r and r + 512/G are
