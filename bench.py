@@ -79,8 +79,11 @@ def pmc_traffic():
     return {"hbm_bytes_per_trial": d["hbm_bytes_per_trial"], "source": src, "commit": d.get("commit")}, "ok"
 
 
-def cpu_baseline(timeout_s=300):
-    cmd = [sys.executable, os.path.join(REPO, "oracle", "cpu_baseline.py")]
+def cpu_baseline(workload="cfg2", cores="", extra=(), timeout_s=400):
+    cmd = [sys.executable, os.path.join(REPO, "oracle", "cpu_baseline.py"), "--workload", workload]
+    if cores:
+        cmd += ["--cores", str(cores)]
+    cmd += list(extra)
     try:
         out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, check=True).stdout
         res = json.loads(out.strip().splitlines()[-1])
@@ -90,61 +93,260 @@ def cpu_baseline(timeout_s=300):
         return {"value": None, "unit": "DM trials/s", "cores": None, "kind": "reference", "sample": f"failed: {e}"}
 
 
+def cpu_baselines(workload, extra=()):
+    """The rffa CPU model on this host: `cpu_baseline` on this process's CPU
+    share (16 cores per GPU on the GPU box), plus `node` on every affinity
+    core (the node-level comparison), each with its core count."""
+    share = cpu_baseline(workload, extra=extra)
+    share["node"] = cpu_baseline(workload, cores="all", extra=extra)
+    return share
+
+
+def roofline(engine, cone, stats, trials_per_launch_unit, pmc=None, pmc_reason=None):
+    """The roofline object of a bench line: Σ algorithmic bytes of the cone
+    launches ÷ Σ their HIP-event durations, against 8 TB/s."""
+    achieved = cone["alg_bytes"] / (cone["ms"] * 1e-3) / 1e9 if cone["ms"] > 0 else None
+    B = trials_per_launch_unit
+    return {
+        "bound": "hbm",
+        "kernel": "cone_kernel (FFA passes + fused boxcar S/N)",
+        "achieved": achieved,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+        "traffic": (pmc["hbm_bytes_per_trial"] * B / stats["launches"]) if pmc else None,
+        "traffic_per_trial": pmc["hbm_bytes_per_trial"] if pmc else None,
+        "traffic_source": pmc["source"] if pmc else None,
+        "traffic_status": pmc_reason,
+        "alg_bytes_per_launch": stats["alg_bytes"] * B / stats["launches"],
+        "alg_bytes_per_trial": stats["alg_bytes"],
+        "moved_bytes_per_trial": stats["moved_bytes"],
+    }
+
+
+def _drop_cache(fn):
+    """fsync the file and drop it from the page cache, so the next read of it
+    comes from the disk (POSIX_FADV_DONTNEED; best effort)."""
+    fd = os.open(fn, os.O_RDONLY)
+    try:
+        os.fsync(fd)
+        os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+    finally:
+        os.close(fd)
+
+
 def bench_cfg5(args, torch, dist, world, rank, local, dev):
     """BASELINE configs[4] (cfg5): SIGPROC .tim DM trials of 2^23 samples @ 64 us
     searched from files to peak lists, the rffa search stage
     (pipeline.py:177-189 with worker_pool.py:47-70) on the GPU worker pool:
     file read + H2D (8-bit files converted on the device) + deredden +
-    normalise + 3 search ranges (example.yaml) + device peak detection, in
-    DMIterator chunks.  Each rank searches its own files (weak scaling)."""
+    normalise + 3 search ranges (example.yaml) + device peak detection.
+    Each rank searches its round-robin share of the node's file list
+    (dispatch.search_files: DMIterator chunks of --batch files, the next chunk
+    read into a bounded page-locked ring while the current one is on the
+    device).  Two timed passes: `cold` after the files were fsync'ed and
+    dropped from the page cache (the reads hit the disk; this is `value`),
+    then `warm` (page cache)."""
+    import shutil
     import tempfile
     sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
     import inputs
+    from riptide_amd.dispatch import search_files
     from riptide_amd.reading import write_sigproc
-    from riptide_amd.worker_pool import GpuWorkerPool, iterate_chunks
+    from riptide_amd.worker_pool import GpuWorkerPool
     c = inputs.CFG5
-    tmp = tempfile.mkdtemp(prefix=f"cfg5_r{rank}_", dir=os.environ.get("TMPDIR", "/tmp"))
-    fnames = []
-    for j in range(args.files):
-        k = rank * args.files + j
-        data, hdr = inputs.cfg5_trial(k % 64)
+    root = os.environ.get("TMPDIR", "/tmp")
+    files = args.files
+    # ~8 MiB (8-bit) / 32 MiB (float32) per file; leave 20 % of the disk free
+    free = shutil.disk_usage(root).free
+    files = max(2 * args.batch, min(files, int(0.8 * free / world / (34 << 20))))
+    tmp = tempfile.mkdtemp(prefix=f"cfg5_r{rank}_", dir=root)
+    # the node's file list (rank r writes the files it will search, k = r, r + world, ...)
+    total = world * files
+    fnames = [None] * total
+    base = {}
+    for k in range(rank, total, world):
+        j = k % 64
+        if j not in base:
+            base[j] = inputs.cfg5_trial(j)
+        data, hdr = base[j]
         fn = os.path.join(tmp, f"DM{hdr['refdm']:08.2f}_{k:05d}.tim")
         write_sigproc(fn, data, hdr)
-        fnames.append(fn)
+        fnames[k] = fn
+    base.clear()
+    for k in range(rank, total, world):
+        _drop_cache(fnames[k])
+    if world > 1:      # every rank's paths (the others' entries are not read by this rank)
+        parts = [None] * world
+        dist.all_gather_object(parts, fnames[rank::world])
+        for r in range(world):
+            fnames[r::world] = parts[r]
     pool = GpuWorkerPool(c["dereddening"], c["ranges"], processes=args.batch, fmt="sigproc", batch=args.batch,
                          device=local)
-    pool.process_fname_list(fnames[:args.batch])          # warmup: plans, device buffers
+    # warmup on a private copy (plans, device buffers, page-locked ring) so the
+    # timed files stay cold
+    wfn = os.path.join(tmp, "warmup.tim")
+    d0, h0 = inputs.cfg5_trial(0)
+    write_sigproc(wfn, d0, h0)
+    pool.process_fname_list([wfn] * min(args.batch, 2))
+    os.remove(wfn)
+    res = {}
+    for mode in ("cold", "warm"):
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        peaks = search_files(fnames, pool, chunksize=args.batch)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        res[mode] = (elapsed, len(peaks))
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        lst = os.path.join(tmp, "files.txt")
+        with open(lst, "w") as f:
+            f.write("\n".join(fnames))
+        cpu = cpu_baselines("cfg5", extra=("--files-from", lst))
+    if world > 1:
+        dist.barrier()
+    for k in range(rank, total, world):
+        os.remove(fnames[k])
+    shutil.rmtree(tmp, ignore_errors=True)
+    if rank == 0:
+        cold, warm = res["cold"], res["warm"]
+        line = {
+            "metric": "DM trials/sec files->peaks (cfg5 rffa search stage, 2^23 samples @ 64 us, 3 ranges)",
+            "value": total / cold[0], "unit": "DM trials/s", "n_gpus": world, "steps": 1, "warmup": 1,
+            "ms_per_step": cold[0] * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32", "data": "synthetic SIGPROC files (tests/golden/inputs.py cfg5_trial k mod 64; 6 of 8 "
+                                    "float32, 2 of 8 8-bit) written, fsync'ed and dropped from the page cache "
+                                    "before the timed region (value: cold reads from disk)",
+            "config": {"workload": "cfg5: rffa search stage on SIGPROC .tim files (example.yaml ranges short / "
+                                   "medium / long, smin 6), dispatch.search_files, DMIterator chunks of --batch "
+                                   "files with the next chunk prefetched",
+                       "files_per_gpu": files, "chunk": args.batch, "peaks_found": cold[1],
+                       "parallelism": f"dm-trials x{world} (independent, weak scaling)"},
+            "cold": {"value": total / cold[0], "seconds": cold[0]},
+            "warm": {"value": total / warm[0], "seconds": warm[0], "peaks_found": warm[1]},
+        }
+        if cpu is not None:
+            line["cpu_baseline"] = cpu
+        print(json.dumps(line), flush=True)
+
+
+CFG3 = dict(n=1 << 22, tsamp=256e-6, pmin=0.2, pmax=5.0, bmin=240, bmax=260, ducy_max=0.2,
+            rmed_width=4.0, rmed_minpts=101, trials=1024)
+
+
+def cfg3_trials(torch, ks, n, tsamp, device):
+    """BASELINE configs[2] trials, generated on the device: trial k is white
+    noise from a generator seeded k, plus a slow red-noise ramp; every 64th
+    trial carries a top-hat pulsar (period 0.2 + 4.8 * frac(0.618 k) s,
+    amplitude 10-20)."""
+    x = torch.empty((len(ks), n), dtype=torch.float32, device=device)
+    g = torch.Generator(device=device)
+    t = torch.arange(n, device=device, dtype=torch.float64) * tsamp
+    ramp = (0.5 * torch.sin(2 * 3.141592653589793 * t / 700.0)).to(torch.float32)
+    for i, k in enumerate(ks):
+        g.manual_seed(k)
+        torch.randn((n,), generator=g, device=device, dtype=torch.float32, out=x[i])
+        x[i] += ramp
+        if k % 64 == 0:
+            period = 0.2 + 4.8 * ((0.6180339887 * k) % 1.0)
+            amp = 10.0 + 10.0 * ((0.7548776662 * k) % 1.0)
+            on = torch.remainder(t / period + 0.3, 1.0) < 0.02
+            x[i] += on.to(torch.float32) * (amp / float(on.sum().item()) ** 0.5)
+    return x
+
+
+def bench_cfg3(args, torch, dist, world, rank, local, dev):
+    """BASELINE configs[2] as configured: a job of 1024 DM trials x 2^22
+    samples @ 256 us (P 0.2-5 s, bins 240-260, 10 widths), strong-sharded
+    over the ranks (dispatch.shard(1024, rank, world), round-robin, no
+    data-path collective), each rank's share resident in HBM.  One step = the
+    whole job: deredden + normalise + periodogram of every trial, in device
+    batches of --batch trials.  value = 1024 x steps / (max over ranks of the
+    timed wall time)."""
+    from riptide_amd import engine
+    from riptide_amd.dispatch import shard
+    c = CFG3
+    ntr = args.trials or c["trials"]
+    mine = shard(ntr, rank, world)
+    B = min(args.batch, max(1, len(mine)))
+    plan = engine.PeriodogramPlan.for_search(c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"],
+                                             ducy_max=c["ducy_max"], device=local)
+    ws_samples = int(round(c["rmed_width"] / c["tsamp"]))
+    X = cfg3_trials(torch, mine, c["n"], c["tsamp"], dev)
+    xbuf = torch.empty((B, c["n"]), dtype=torch.float32, device=dev)
+    dws = torch.empty(engine.deredden_workspace_bytes(c["n"], ws_samples, c["rmed_minpts"], B),
+                      dtype=torch.uint8, device=dev)
+    snr = torch.empty((B, plan.length, plan.num_widths), dtype=torch.float32, device=dev)
+    pws = torch.empty(plan.workspace_bytes(B), dtype=torch.uint8, device=dev)
+
+    def job():
+        for b0 in range(0, len(mine), B):
+            b1 = min(b0 + B, len(mine))
+            engine.deredden_normalise(X[b0:b1], ws_samples, c["rmed_minpts"], out=xbuf[:b1 - b0], workspace=dws)
+            plan.run(xbuf[:b1 - b0], out=snr[:b1 - b0], workspace=pws)
+
+    for _ in range(args.warmup):
+        job()
     torch.cuda.synchronize()
+    plan.check()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    engine.profile_reset()
+    engine.profile_enable(True)
     t0 = time.perf_counter()
-    npeaks = 0
-    for chunk in iterate_chunks(fnames, chunksize=args.batch):
-        npeaks += len(pool.process_fname_list(chunk))
+    for _ in range(args.steps):
+        job()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    engine.profile_enable(False)
+    plan.check()
     if world > 1:
         dist.barrier()
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    for fn in fnames:
-        os.remove(fn)
-    os.rmdir(tmp)
+    cone = engine.profile_read(0)
+    stats = plan.stats()
     if rank == 0:
-        trials = world * args.files
-        print(json.dumps({
-            "metric": "DM trials/sec files->peaks (cfg5 rffa search stage, 2^23 samples @ 64 us, 3 ranges)",
-            "value": trials / elapsed, "unit": "DM trials/s", "n_gpus": world, "steps": 1, "warmup": 1,
-            "ms_per_step": elapsed * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f32", "data": "synthetic SIGPROC files (tests/golden/inputs.py cfg5_trial; 6 of 8 float32, "
-                                    "2 of 8 8-bit) written to local disk before the timed region",
-            "config": {"workload": "cfg5: rffa search stage on SIGPROC .tim files (example.yaml ranges short / "
-                                   "medium / long, smin 6), DMIterator chunks of --batch files",
-                       "files_per_gpu": args.files, "chunk": args.batch, "peaks_found": npeaks,
-                       "parallelism": f"dm-trials x{world} (independent, weak scaling)"},
-        }), flush=True)
+        rf = roofline(engine, cone, stats, B)
+        rf["kernel_ms_per_trial"] = cone["ms"] / (args.steps * len(mine))
+        line = {
+            "metric": "DM trials/sec (node), 1024-trial job at 2^22 samples, P=0.2-5 s (BASELINE configs[2])",
+            "value": ntr * args.steps / elapsed,
+            "unit": "DM trials/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (device-generated white noise + red-noise ramp, a top-hat pulsar in every 64th "
+                    "trial; each rank's share resident in HBM)",
+            "config": {
+                "workload": "cfg3: 1024 DM trials x 2^22 samples @ 256 us, deredden(4 s, 101 pts) + normalise + "
+                            "FFA periodogram P=0.2-5 s, bins 240-260, 10 widths; one step = the whole job",
+                "trials_total": ntr, "trials_per_gpu": len(mine), "batch": B,
+                "trial_periods": plan.length, "ffa_transforms": stats["transforms"],
+                "cone_launches_per_batch": stats["launches"],
+                "parallelism": f"dm-trials x{world} (round-robin shard of one job, strong scaling)",
+            },
+            "roofline": rf,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baselines("cfg3")
+        print(json.dumps(line), flush=True)
 
 
 def main():
@@ -152,17 +354,22 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=16, help="DM trials per GPU per step")
-    ap.add_argument("--workload", choices=("cfg2", "cfg5"), default="cfg2",
-                    help="cfg2: headline periodogram throughput (device-resident); cfg5: files -> peaks")
-    ap.add_argument("--files", type=int, default=32, help="cfg5: SIGPROC files per GPU")
+    ap.add_argument("--batch", type=int, default=0, help="DM trials per GPU per device batch "
+                                                           "(default: 16 cfg2 / cfg5, 32 cfg3)")
+    ap.add_argument("--workload", choices=("cfg2", "cfg3", "cfg5"), default="cfg2",
+                    help="cfg2: headline periodogram throughput (device-resident, weak scaling); cfg3: the "
+                         "1024-trial job of BASELINE configs[2] (strong scaling); cfg5: files -> peaks")
+    ap.add_argument("--files", type=int, default=256, help="cfg5: SIGPROC files per GPU")
+    ap.add_argument("--trials", type=int, default=0, help="cfg3: trials in the job (default 1024)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    if not args.batch:
+        args.batch = 32 if args.workload == "cfg3" else 16
 
     # transform-group scratch per ping/pong buffer and trial (capi.cpp
     # scratch_budget_floats): 384 M floats = 26 instead of 94 cone launches per
     # step, ~1 % faster (tools/ab_sched.py); 49 GB of the 288 GB HBM at 16 trials
-    if args.workload == "cfg2":
+    if args.workload in ("cfg2", "cfg3"):
         os.environ.setdefault("RIPTIDE_AMD_SCRATCH_MFLOATS", "384")
     import torch
     import torch.distributed as dist
@@ -175,8 +382,8 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-    if args.workload == "cfg5":
-        bench_cfg5(args, torch, dist, world, rank, local, dev)
+    if args.workload in ("cfg3", "cfg5"):
+        (bench_cfg3 if args.workload == "cfg3" else bench_cfg5)(args, torch, dist, world, rank, local, dev)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -225,7 +432,10 @@ def main():
     if rank == 0:
         pmc, pmc_reason = pmc_traffic()
         trials = world * B * args.steps
-        achieved = cone["alg_bytes"] / (cone["ms"] * 1e-3) / 1e9 if cone["ms"] > 0 else None
+        rf = roofline(engine, cone, stats, B, pmc, pmc_reason)
+        rf["kernel_ms_per_step"] = cone["ms"] / args.steps
+        rf["kernel_launches_per_step"] = cone["launches"] / args.steps
+        rf["ladder_ms_per_step"] = ladder["ms"] / args.steps
         line = {
             "metric": METRIC,
             "value": trials / elapsed,
@@ -249,27 +459,10 @@ def main():
                 "scratch_mfloats_per_buffer_trial": float(os.environ["RIPTIDE_AMD_SCRATCH_MFLOATS"]),
                 "parallelism": f"dm-trials x{world} (independent, weak scaling)",
             },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "cone_kernel (FFA passes + fused boxcar S/N)",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                "traffic": (pmc["hbm_bytes_per_trial"] * B / stats["launches"]) if pmc else None,
-                "traffic_per_trial": pmc["hbm_bytes_per_trial"] if pmc else None,
-                "traffic_source": pmc["source"] if pmc else None,
-                "traffic_status": pmc_reason,
-                "alg_bytes_per_launch": stats["alg_bytes"] * B / stats["launches"],
-                "alg_bytes_per_trial": stats["alg_bytes"],
-                "moved_bytes_per_trial": stats["moved_bytes"],
-                "kernel_ms_per_step": cone["ms"] / args.steps,
-                "kernel_launches_per_step": cone["launches"] / args.steps,
-                "ladder_ms_per_step": ladder["ms"] / args.steps,
-            },
+            "roofline": rf,
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline()
+            line["cpu_baseline"] = cpu_baselines("cfg2")
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

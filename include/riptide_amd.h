@@ -216,6 +216,13 @@ int rt_diag_timeline(uint64_t* out, uint64_t cap, uint64_t* count);
 int rt_plan_stats(const rt_plan* plan, uint64_t* transforms, uint64_t* items, uint64_t* launches,
                   double* alg_bytes_per_trial, double* moved_bytes_per_trial, uint64_t* cells_per_trial);
 
+/* TEST ONLY (no reference counterpart): while `on` is non-zero, every plan
+ * uploaded to a device carries one unit that breaks the cone kernel's budget,
+ * so the kernel refuses it and raises the plan's error flag -- exercises
+ * rt_plan_check and the host-buffer API's error path.  The product never sets
+ * it; tests/test_gpu_e2e.py::test_plan_device_error_flag does. */
+int rt_test_corrupt_next_plans(int on);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,6 +1,6 @@
 """CPU baseline for bench.py (TEST INFRASTRUCTURE, run in a subprocess).
 
-The rffa CPU model (riptide/pipeline/worker_pool.py:35-45 and
+The rffa CPU model (riptide/pipeline/worker_pool.py:35-70 and
 pipeline.py:508): a multiprocessing.Pool of C worker processes, one DM trial
 per process, BLAS pinned to one thread; each trial is dereddened and
 normalised (numpy, restated in oracle.py from time_series.py:66-122), then
@@ -10,11 +10,21 @@ oracle/_ref/portable = x86-64-v3 otherwise -> kind "reference"; the clean-room
 C restatement when neither is present -> kind "port"), then run through
 find_peaks (riptide_amd.peak_detection, the reference's numpy expressions).
 
-C = the worker processes actually used: the CPU share this process may use
-(sched_getaffinity, capped by OMP_NUM_THREADS where the harness sets it, as on
-the GPU box: 16 host cores per GPU).  Reports the search-only rate (deredden
-+ normalise + periodogram: the work bench.py's GPU step does) as `value`, and
-search + find_peaks separately.  Prints one JSON object.
+Workloads (bench.py legs):
+  cfg2  one 2^23-sample trial per process (P 0.1-10 s, bins 240-260, W 6);
+  cfg3  one 2^22-sample trial per process (P 0.2-5 s, bins 240-260, W 10);
+  cfg5  SIGPROC files (--files-from, one path a line) searched like
+        WorkerPool.process_fname: read, deredden + normalise once, then every
+        example.yaml range (periodogram + find_peaks).
+
+C = the worker processes used: `--cores N`, `--cores all` (every core of
+sched_getaffinity -- the node-level comparison), or by default this process's
+CPU share (sched_getaffinity capped by OMP_NUM_THREADS where the harness sets
+it: 16 host cores per GPU on the GPU box).  Workers are also capped so their
+resident memory (measured ~0.5 GB per cfg2 trial) stays within half of the
+available memory and 120 GB.  Reports the search-only rate (deredden + normalise +
+periodogram: the work bench.py's GPU step does) as `value`, and search +
+find_peaks separately.  Prints one JSON object.
 """
 import argparse
 import glob
@@ -35,6 +45,16 @@ sys.path.insert(0, os.path.dirname(HERE))
 _A = None            # parsed arguments (inherited by the forked workers)
 _PGRAM = None
 _KIND = None
+_FILES = []
+
+WORKLOADS = {
+    "cfg2": dict(n=1 << 23, tsamp=256e-6, pmin=0.1, pmax=10.0, bmin=240, bmax=260, ducy_max=0.05),
+    "cfg3": dict(n=1 << 22, tsamp=256e-6, pmin=0.2, pmax=5.0, bmin=240, bmax=260, ducy_max=0.2),
+}
+# cfg5: tests/golden/inputs.py CFG5 (example.yaml's dereddening and ranges)
+CFG5_DEREDDEN = (5.0, 101)
+CFG5_RANGES = [(0.2, 0.5, 240, 260), (0.5, 2.0, 480, 520), (2.0, 120.0, 960, 1040)]
+RSS_GB = {"cfg2": 0.55, "cfg3": 0.35, "cfg5": 0.9}
 
 
 def _avx512():
@@ -62,22 +82,51 @@ def _load_pgram():
 
 
 def _trial(k):
-    """One DM trial (process_fname model): returns absolute timestamps
-    (start, search done, peaks done) after the untimed input generation."""
+    """One synthetic DM trial (process_fname model): returns absolute
+    timestamps (start, search done, peaks done) after the untimed input
+    generation."""
     from oracle import oracle as O
     from riptide_amd.peak_detection import find_peaks
     from riptide_amd.periodogram import Periodogram
-    a = _A
-    raw = np.random.RandomState(1234 + k).normal(size=a.n).astype(np.float32)
-    widths = O.generate_width_trials(a.bmin, a.ducy_max)
+    c = WORKLOADS[_A.workload]
+    raw = np.random.RandomState(1234 + k).normal(size=c["n"]).astype(np.float32)
+    widths = O.generate_width_trials(c["bmin"], c["ducy_max"])
     t0 = time.time()
-    x = O.normalise(O.deredden(raw, a.tsamp, 4.0, 101))
-    periods, foldbins, snrs = _PGRAM(x, a.tsamp, widths, a.pmin, a.pmax, a.bmin, a.bmax)
+    x = O.normalise(O.deredden(raw, c["tsamp"], 4.0, 101))
+    periods, foldbins, snrs = _PGRAM(x, c["tsamp"], widths, c["pmin"], c["pmax"], c["bmin"], c["bmax"])
     t1 = time.time()
-    pg = Periodogram(widths, periods, foldbins, snrs, metadata={"tobs": a.n * a.tsamp, "dm": float(k)})
+    pg = Periodogram(widths, periods, foldbins, snrs, metadata={"tobs": c["n"] * c["tsamp"], "dm": float(k)})
     find_peaks(pg)
     t2 = time.time()
     return t0, t1, t2
+
+
+def _file(k):
+    """WorkerPool.process_fname (worker_pool.py:47-70) on file k: the read is
+    inside the timed region, as in rffa; the search time (read + deredden +
+    normalise + periodograms) and the find_peaks time are kept apart."""
+    from oracle import oracle as O
+    from riptide_amd.peak_detection import find_peaks
+    from riptide_amd.periodogram import Periodogram
+    from riptide_amd.reading import read_sigproc
+    t0 = time.time()
+    data, meta, tsamp = read_sigproc(_FILES[k])
+    x = O.normalise(O.deredden(np.asarray(data, np.float32), tsamp, *CFG5_DEREDDEN))
+    tobs = x.size * tsamp
+    search = peaks = 0.0
+    for pmin, pmax, bmin, bmax in CFG5_RANGES:
+        a = time.time()
+        widths = O.generate_width_trials(bmin, 0.2, 1.5)
+        periods, foldbins, snrs = _PGRAM(x, tsamp, widths, pmin, pmax, bmin, bmax)
+        b = time.time()
+        find_peaks(Periodogram(widths, periods, foldbins, snrs, metadata={"tobs": tobs, "dm": meta.get("dm")}),
+                   smin=6.0)
+        search += b - a
+        peaks += time.time() - b
+    t1 = time.time()
+    # (start, search done, peaks done) on the trial's own clock: find_peaks
+    # time moved to the end so the search stamp counts read + search only
+    return t0, t1 - peaks, t1
 
 
 def default_cores():
@@ -89,27 +138,55 @@ def default_cores():
     return c
 
 
+def _mem_available_gb():
+    try:
+        with open("/proc/meminfo") as f:
+            for line in f:
+                if line.startswith("MemAvailable:"):
+                    return int(line.split()[1]) / 2 ** 20
+    except OSError:
+        pass
+    return None
+
+
 def main():
-    global _A, _PGRAM, _KIND
+    global _A, _PGRAM, _KIND, _FILES
     ap = argparse.ArgumentParser()
-    ap.add_argument("--n", type=int, default=1 << 23)
-    ap.add_argument("--tsamp", type=float, default=256e-6)
-    ap.add_argument("--pmin", type=float, default=0.1)
-    ap.add_argument("--pmax", type=float, default=10.0)
-    ap.add_argument("--bmin", type=int, default=240)
-    ap.add_argument("--bmax", type=int, default=260)
-    ap.add_argument("--ducy-max", type=float, default=0.05)
-    ap.add_argument("--cores", type=int, default=0, help="worker processes (default: this process's CPU share)")
+    ap.add_argument("--workload", choices=("cfg2", "cfg3", "cfg5"), default="cfg2")
+    ap.add_argument("--cores", default="", help="worker processes: N, 'all' (every affinity core), "
+                                                "default this process's CPU share")
     ap.add_argument("--trials-per-core", type=int, default=1)
+    ap.add_argument("--files-from", default="", help="cfg5: text file with one SIGPROC path per line")
     _A = ap.parse_args()
-    cores = _A.cores or default_cores()
+    affinity = len(os.sched_getaffinity(0))
+    if _A.cores == "all":
+        cores = affinity
+    elif _A.cores:
+        cores = int(_A.cores)
+    else:
+        cores = default_cores()
+    mem = _mem_available_gb()
+    mem_cap = None
+    if mem:
+        # half the available memory, at most 120 GB (the GPU box's per-command cap is 270 GB)
+        mem_cap = max(1, int(min(0.5 * mem, 120.0) / RSS_GB[_A.workload]))
+        cores = min(cores, mem_cap)
     for var in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):   # threadpool_limits(1)
         os.environ[var] = "1"
-    ntrials = cores * _A.trials_per_core
     _PGRAM, _KIND, what = _load_pgram()
+    if _A.workload == "cfg5":
+        with open(_A.files_from) as f:
+            _FILES = [l.strip() for l in f if l.strip()]
+        ntrials = min(len(_FILES), cores * _A.trials_per_core)
+        work, unit = _file, "SIGPROC file(s) of cfg5 (2^23 samples @ 64 us), read + 3 example.yaml ranges"
+    else:
+        ntrials = cores * _A.trials_per_core
+        work = _trial
+        c = WORKLOADS[_A.workload]
+        unit = f"{_A.workload} trial(s) of {c['n']} samples"
     ctx = multiprocessing.get_context("fork")
     with ctx.Pool(processes=cores) as pool:
-        stamps = pool.map(_trial, range(ntrials), chunksize=1)
+        stamps = pool.map(work, range(ntrials), chunksize=1)
     start = min(s[0] for s in stamps)
     search_wall = max(s[1] for s in stamps) - start
     total_wall = max(s[2] for s in stamps) - start
@@ -117,10 +194,10 @@ def main():
         "value": ntrials / search_wall, "unit": "DM trials/s", "cores": cores, "kind": _KIND,
         "search_and_peaks_per_s": ntrials / total_wall,
         "per_core_search_per_s": ntrials / search_wall / cores,
-        "sample": f"{ntrials} cfg2 trial(s) of {_A.n} samples, multiprocessing.Pool({cores}) one trial per "
-                  f"process (rffa worker-pool model): numpy deredden+normalise + {what} periodogram = value; "
-                  f"+ find_peaks = search_and_peaks_per_s; host CPU share {len(os.sched_getaffinity(0))} "
-                  f"affinity cores",
+        "sample": f"{ntrials} {unit}, multiprocessing.Pool({cores}) one trial per process (rffa worker-pool "
+                  f"model): numpy deredden+normalise + {what} periodogram = value; + find_peaks = "
+                  f"search_and_peaks_per_s; {affinity} affinity cores on this host"
+                  + (f", workers capped at {mem_cap} by available memory" if mem_cap and mem_cap < affinity else ""),
         "seconds": total_wall}))
 
 

@@ -67,6 +67,7 @@ _SIGNATURES = {
     "rt_segment_order_stats_device": (_c_i, [_vp, _c_sz, _c_sz, _c_sz, _c_sz, _c_sz, _c_sz, _vp, _c_sz, _vp, _vp]),
     "rt_threshold_select_device": (_c_i, [_vp, _c_sz, _c_sz, _c_sz, _c_sz, _vp, _vp, _c_sz, _c_d, _vp, _vp, _c_sz,
                                           _vp]),
+    "rt_test_corrupt_next_plans": (_c_i, [_c_i]),   # test-only hook (tests/test_gpu_e2e.py)
 }
 
 EXPORTED = tuple(_SIGNATURES)

@@ -152,6 +152,10 @@ struct Profiler {
     }
 } g_prof;
 
+// test-only: plans uploaded while set carry one corrupt unit (never set by
+// the product; tests toggle it through rt_test_corrupt_next_plans)
+std::atomic<int> g_test_corrupt{0};
+
 // ---- a compiled plan resident on one device
 struct DevicePlan {
     ExecPlan ex;
@@ -198,17 +202,16 @@ struct DevicePlan {
             }
             u[i] = d;
         }
-        // Test hook (RIPTIDE_AMD_DEBUG_CORRUPT_UNIT=1): give the first whole-node
-        // unit more merge levels than any kernel instance runs, after the host
-        // validation, so the kernel's own check refuses it and sets the error
-        // flag (exercises rt_plan_check).
-        if (const char* e = std::getenv("RIPTIDE_AMD_DEBUG_CORRUPT_UNIT"))
-            if (std::atoi(e) != 0)
-                for (UnitDesc& d : u)
-                    if (d.mode == kModeWhole) {
-                        d.levels = kMaxLevels + 1;
-                        break;
-                    }
+        // test-only hook (rt_test_corrupt_next_plans): give the first
+        // whole-node unit more merge levels than any kernel instance runs,
+        // after the host validation, so the kernel's own check refuses it and
+        // sets the error flag (exercises rt_plan_check)
+        if (g_test_corrupt.load(std::memory_order_relaxed))
+            for (UnitDesc& d : u)
+                if (d.mode == kModeWhole) {
+                    d.levels = kMaxLevels + 1;
+                    break;
+                }
         ck(hipMalloc(&d_blob, std::max<size_t>(4, ex.blob.size()) * sizeof(uint32_t)), "hipMalloc");
         if (!ex.blob.empty())
             ck(hipMemcpy(d_blob, ex.blob.data(), ex.blob.size() * sizeof(uint32_t), hipMemcpyHostToDevice),
@@ -1177,3 +1180,9 @@ int rt_plan_stats(const rt_plan* P, uint64_t* transforms, uint64_t* items, uint6
 }
 
 }  // extern "C"
+
+int rt_test_corrupt_next_plans(int on)
+{
+    g_test_corrupt.store(on ? 1 : 0, std::memory_order_relaxed);
+    return RT_OK;
+}

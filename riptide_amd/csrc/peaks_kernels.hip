@@ -16,6 +16,8 @@
 // Both kernels read the periodogram in the engine's [trial][L][W] layout.
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 #include <cstdint>
 
 #include "kernels.hpp"
@@ -106,13 +108,22 @@ hipError_t launch_segment_order_stats(const float* snrs, uint64_t snr_stride, ui
         hipLaunchKernelGGL(segment_order_stats_kernel<kPeakBlock>, dim3(nseg, W, batch), dim3(kPeakBlock), lds, s,
                            snrs, snr_stride, W, per_seg, n2, rk, nranks, out);
     } else {
-        static bool attr = false;    // > 64 KiB of dynamic LDS: opt in once
-        if (!attr) {
-            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(segment_order_stats_kernel<1024>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                     (int)(kMaxSegmentPoints * sizeof(float)));
-            if (e != hipSuccess) return e;
-            attr = true;
+        // > 64 KiB of dynamic LDS: opt in once per device (the attribute is
+        // per device; a mutex so concurrent host threads do not race)
+        static std::mutex mu;
+        static uint64_t done = 0;   // bit d: device d opted in
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return e;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            if (dev >= 64 || !(done >> dev & 1)) {
+                e = hipFuncSetAttribute(reinterpret_cast<const void*>(segment_order_stats_kernel<1024>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)(kMaxSegmentPoints * sizeof(float)));
+                if (e != hipSuccess) return e;
+                if (dev < 64) done |= 1ull << dev;
+            }
         }
         hipLaunchKernelGGL(segment_order_stats_kernel<1024>, dim3(nseg, W, batch), dim3(1024), lds, s, snrs,
                            snr_stride, W, per_seg, n2, rk, nranks, out);

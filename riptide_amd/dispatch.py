@@ -127,23 +127,63 @@ class EngineSearcher:
                                    [t.metadata for t in trials])
 
 
-def search_trials(trials, searcher, group=None):
-    """Search this rank's share of `trials` with `searcher` (a callable taking
-    a list of Trial and returning one peak list per trial, in order); gather
-    every rank's lists.  Returns the full peak list on every rank, in trial
-    order (then range order within a trial): the WorkerPool contract."""
+def _rank_world(group):
     import torch.distributed as dist
-    distributed = dist.is_available() and dist.is_initialized()
-    rank = dist.get_rank(group) if distributed else 0
-    world = dist.get_world_size(group) if distributed else 1
-    mine = shard(len(trials), rank, world)
-    local = searcher([trials[i] for i in mine]) if mine else []
-    if len(local) != len(mine):
-        raise RuntimeError("searcher must return one peak list per trial")
-    tagged = [(i, [tuple(p) for p in plist]) for i, plist in zip(mine, local)]
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(group), dist.get_world_size(group)
+    return 0, 1
+
+
+def _gather_tagged(tagged, group, world):
+    """All ranks' (trial index, peak tuples) lists, gathered once (KB-scale),
+    in trial order, flattened to the WorkerPool contract."""
     if world > 1:
+        import torch.distributed as dist
         gathered = [None] * world
         dist.all_gather_object(gathered, tagged, group=group)
         tagged = [t for part in gathered for t in part]
     tagged.sort(key=lambda t: t[0])
     return [Peak(*p) for _, plist in tagged for p in plist]
+
+
+def search_trials(trials, searcher, group=None, loader=None, chunksize=None):
+    """Search this rank's share of the DM trials with `searcher` (a callable
+    taking a list of Trial and returning one peak list per trial, in order)
+    and gather every rank's lists.  Returns the full peak list on every
+    rank, in trial order (then range order within a trial): the WorkerPool
+    contract (worker_pool.py:35-45).
+
+    `trials` is a sequence of Trial, or -- with `loader` -- the number of
+    trials, `loader(i)` returning Trial i: each rank then loads only its own
+    shard, `chunksize` trials at a time (default: the searcher's batch), so no
+    rank ever holds the whole list."""
+    rank, world = _rank_world(group)
+    n = int(trials) if loader is not None else len(trials)
+    get = loader if loader is not None else (lambda i: trials[i])
+    mine = shard(n, rank, world)
+    cs = int(chunksize or getattr(searcher, "batch", 0) or max(1, len(mine)))
+    tagged = []
+    for c0 in range(0, len(mine), cs):
+        idx = mine[c0:c0 + cs]
+        local = searcher([get(i) for i in idx])
+        if len(local) != len(idx):
+            raise RuntimeError("searcher must return one peak list per trial")
+        tagged += [(i, [tuple(p) for p in plist]) for i, plist in zip(idx, local)]
+    return _gather_tagged(tagged, group, world)
+
+
+def search_files(fnames, pool, group=None, chunksize=None):
+    """rffa's search stage over the ranks of one node (pipeline.py:177-189 with
+    dmiter.py:231-243): each rank searches its round-robin share of the
+    DM-ordered file list through `pool` (a GpuWorkerPool) in chunks of
+    `chunksize` files (default: the pool's batch), the next chunk read into
+    a bounded page-locked ring while the current one is on the device
+    (GpuWorkerPool.search_chunks); one gather of the tagged peak lists.
+    Returns the full peak list on every rank, in file order."""
+    rank, world = _rank_world(group)
+    fnames = list(fnames)
+    mine = shard(len(fnames), rank, world)
+    tagged = []
+    for first, per_file in pool.search_chunks([fnames[i] for i in mine], chunksize=chunksize):
+        tagged += [(mine[first + j], [tuple(p) for p in plist]) for j, plist in enumerate(per_file)]
+    return _gather_tagged(tagged, group, world)

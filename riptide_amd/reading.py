@@ -349,16 +349,20 @@ def upload_samples(raws, device=None, stream=None):
     with torch.cuda.stream(s):
         out = torch.empty((len(raws), n), dtype=torch.float32, device=dev)
         for b, raw in enumerate(raws):
+            raw = np.asarray(raw)
+            if raw.dtype != np.float32 and raw.dtype not in kinds:
+                raw = raw.astype(np.float32)      # e.g. float64 series (EngineSearcher's old cast)
             raw = np.ascontiguousarray(raw)
-            # non_blocking: an asynchronous DMA when the samples sit in
-            # page-locked memory (_raw_samples' staging); the caller keeps
-            # that memory until the stream has consumed it
+            src = torch.from_numpy(raw if raw.dtype == np.float32 else raw.view(np.uint8))
+            # asynchronous only from page-locked memory (_raw_samples' staging
+            # slots, whose owner waits for the stream before refilling them);
+            # pageable sources (and temporaries made here) are copied
+            # synchronously, so nothing dropped below is still being read
+            pinned = src.is_pinned()
             if raw.dtype == np.float32:
-                out[b].copy_(torch.from_numpy(raw), non_blocking=True)
+                out[b].copy_(src, non_blocking=pinned)
                 continue
-            if raw.dtype not in kinds:
-                raise ValueError(f"unsupported sample type {raw.dtype}")
-            staged = torch.from_numpy(raw.view(np.uint8)).to(dev, non_blocking=True)
+            staged = src.to(dev, non_blocking=pinned)
             _lib.check(L.rt_convert_samples_device(_lib.ptr(staged), n, kinds[raw.dtype], _lib.ptr(out[b]),
                                                    _stream_handle(s)))
     return out

@@ -12,8 +12,15 @@ compiled plan per range and series shape) and device peak detection
 (riptide_amd.peaks).  Peaks come back per file in input order and, within a
 file, in range order -- the order WorkerPool.process_fname_list returns them
 in.
+
+Long file lists (a rank's share of a beam, dmiter.py:231-243 chunks) go
+through `search_chunks`: a reader thread reads chunk k + 1 into one half of a
+fixed ring of page-locked slots while chunk k is searched from the other
+half, so host memory stays at 2 x chunk files whatever the list length and
+file reads overlap the device work.
 """
 import logging
+import threading
 
 from .dispatch import EngineSearcher
 from .reading import _raw_samples
@@ -52,16 +59,19 @@ class GpuWorkerPool:
         self.processes = int(processes)
         self.fmt = fmt
         self.batch = int(batch)
+        self.device = device
         self.searcher = EngineSearcher(self.deredden_params, self.range_confs, device=device, batch=self.batch)
+        self._pinned = {}
+        # per ring half: a device event recorded after the half's samples were
+        # last consumed; a half is refilled only after its event completed
+        self._half_done = {}
 
     def _stager(self, slot):
-        """staging(nbytes) for file slot `slot` of a chunk: a page-locked
-        uint8 buffer, grown when a file needs more (None without a GPU)."""
+        """staging(nbytes) for ring slot `slot` = (half, file index): a page-locked uint8 buffer,
+        grown when a file needs more (None without a GPU or for PRESTO)."""
         import torch
-        if not torch.cuda.is_available():
+        if self.fmt != "sigproc" or not torch.cuda.is_available():
             return None
-        if not hasattr(self, "_pinned"):
-            self._pinned = {}
 
         def staging(nbytes):
             buf = self._pinned.get(slot)
@@ -71,29 +81,87 @@ class GpuWorkerPool:
             return buf.numpy()
         return staging
 
-    def process_fname(self, fname):
-        return self.process_fname_list([fname])
+    def _wait_half(self, half):
+        ev = self._half_done.pop(half, None)
+        if ev is not None:
+            ev.synchronize()
 
-    def process_fname_list(self, fnames):
-        # the chunk's files are read concurrently (np.fromfile releases the
-        # GIL), as rffa's pool reads one file per process
-        fnames = list(fnames)
-        # SIGPROC samples land in page-locked slots reused across chunks (one
-        # per file of a chunk), so the uploads are asynchronous DMAs; every
-        # device use of a chunk's samples has completed when search_samples
-        # returns (its peak lists are on the host), before the slots are
-        # refilled by the next call
-        stagers = [self._stager(i) for i in range(len(fnames))] if self.fmt == "sigproc" else [None] * len(fnames)
+    def _release_half(self, half):
+        """Record that the device work reading ring half `half` is queued:
+        the next fill of the half waits for it (search_samples happens to
+        synchronise when its peaks reach the host; this does not rely on it)."""
+        import torch
+        if not torch.cuda.is_available():
+            return
+        dev = torch.device("cuda", torch.cuda.current_device() if self.device is None else self.device)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        self._half_done[half] = ev
+
+    def _read(self, fnames, half):
+        """Read a chunk's files (concurrently: np.fromfile / readinto release
+        the GIL) into ring half `half`.  Returns (raws, metas, tsamps)."""
+        self._wait_half(half)
+        stagers = [self._stager((half, i)) for i in range(len(fnames))]
         if len(fnames) > 1:
             from concurrent.futures import ThreadPoolExecutor
             with ThreadPoolExecutor(max_workers=min(len(fnames), _READ_THREADS)) as ex:
                 loaded = list(ex.map(lambda a: _raw_samples(a[0], self.fmt, staging=a[1]), zip(fnames, stagers)))
         else:
             loaded = [_raw_samples(fn, self.fmt, staging=st) for fn, st in zip(fnames, stagers)]
-        raws = [t[0] for t in loaded]
-        metas = [t[1] for t in loaded]
-        tsamps = [t[2] for t in loaded]
-        per_file = self.searcher.search_samples(raws, tsamps, metas)
+        return [t[0] for t in loaded], [t[1] for t in loaded], [t[2] for t in loaded]
+
+    def _search(self, loaded, half):
+        raws, metas, tsamps = loaded
+        try:
+            per_file = self.searcher.search_samples(raws, tsamps, metas)
+        finally:
+            self._release_half(half)
         for meta, peaks in zip(metas, per_file):
             log.debug(f"Done searching DM = {meta.get('dm')}, peaks found: {len(peaks)}")
+        return per_file
+
+    def process_fname(self, fname):
+        return self.process_fname_list([fname])
+
+    def process_fname_list(self, fnames):
+        """WorkerPool.process_fname_list: one chunk, read then searched."""
+        fnames = list(fnames)
+        per_file = self._search(self._read(fnames, 0), 0)
         return [p for plist in per_file for p in plist]
+
+    def search_chunks(self, fnames, chunksize=None):
+        """Search a long file list chunk by chunk (DMIterator chunks of
+        `chunksize`, default `batch`), yielding (first index, per-file peak
+        lists) per chunk in order.  Chunk k + 1 is read by a background
+        thread into the other half of the page-locked ring while chunk k is
+        on the device; at most two chunks of samples are held at any time."""
+        fnames = list(fnames)
+        cs = int(chunksize or self.batch)
+        chunks = [(i, fnames[i:i + cs]) for i in range(0, len(fnames), cs)]
+        if not chunks:
+            return
+        box = {}
+
+        def reader(k):
+            try:
+                box[k] = self._read(chunks[k][1], k % 2)
+            except BaseException as e:   # re-raised in the searching thread
+                box[k] = e
+
+        th = threading.Thread(target=reader, args=(0,), daemon=True)
+        th.start()
+        try:
+            for k, (first, _) in enumerate(chunks):
+                th.join()
+                loaded = box.pop(k)
+                if isinstance(loaded, BaseException):
+                    raise loaded
+                if k + 1 < len(chunks):
+                    # the next chunk's half was last read by chunk k - 1,
+                    # whose device event _read waits for before refilling it
+                    th = threading.Thread(target=reader, args=(k + 1,), daemon=True)
+                    th.start()
+                yield first, self._search(loaded, k % 2)
+        finally:
+            th.join()      # no reader left writing into the ring

@@ -99,3 +99,67 @@ def test_search_trials_restores_trial_order():
         return [[Peak(1.0, 1.0, 1, 0.1, 0, k, 7.0, t.metadata["dm"])] for k, t in enumerate(ts)]
     out = search_trials(trials, fake)
     assert [p.dm for p in out] == [t.metadata["dm"] for t in trials]
+
+
+class _FakePool:
+    """GpuWorkerPool.search_chunks contract without a GPU: one peak per file
+    whose dm is parsed from the file name; records the chunk sizes."""
+
+    def __init__(self):
+        self.chunks = []
+
+    def search_chunks(self, fnames, chunksize=None):
+        from riptide_amd.peak_detection import Peak
+        cs = chunksize or 3
+        for i in range(0, len(fnames), cs):
+            part = fnames[i:i + cs]
+            self.chunks.append(len(part))
+            yield i, [[Peak(1.0, 1.0, 1, 0.1, 0, 0, 7.0, float(fn.split("_")[1]))] for fn in part]
+
+
+def _files_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from riptide_amd.dispatch import search_files, search_trials
+        pool = _FakePool()
+        fn = [f"f_{k}" for k in range(11)]
+        peaks = search_files(fn, pool, chunksize=2)
+        # loader form: each rank loads only its own shard
+        loaded = []
+        trials = make_trials()
+
+        def loader(i):
+            loaded.append(i)
+            return trials[i]
+        tp = search_trials(len(trials), oracle_searcher, loader=loader, chunksize=2)
+        q.put((rank, [p.dm for p in peaks], pool.chunks, sorted(loaded), [tuple(p) for p in tp]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_search_files_and_loader_world2():
+    """search_files shards the file list round-robin, feeds each rank's share
+    to the pool in chunks, and gathers the per-file lists back in file order;
+    search_trials with a loader loads only the rank's own trials."""
+    from riptide_amd.dispatch import search_trials
+    single = [tuple(p) for p in search_trials(make_trials(), oracle_searcher)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_files_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r = q.get(timeout=300)
+        res[r[0]] = r[1:]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank in (0, 1):
+        dms, chunks, loaded, tp = res[rank]
+        assert dms == [float(k) for k in range(11)]                 # file order on every rank
+        assert chunks == ([2, 2, 2] if rank == 0 else [2, 2, 1])     # 6 / 5 files in chunks of 2
+        assert loaded == list(range(rank, 7, 2))                     # only the rank's own trials
+        assert tp == single

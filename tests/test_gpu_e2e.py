@@ -141,7 +141,8 @@ def _cfg5_files(tmp_path, e2e):
     for f in e2e["cfg5"]["files"]:
         data, hdr = inputs.cfg5_trial(f["k"])
         if sha(data) != f["input_sha"]:
-            pytest.skip("cfg5 input generator differs on this host; parity not checkable")
+            pytest.fail(f"cfg5 input generator drifted on this host: input sha256 {sha(data)} != golden "
+                        f"{f['input_sha']}; the cfg5 parity check cannot run")
         fn = str(tmp_path / f"cfg5_DM{hdr['refdm']:06.1f}.tim")
         write_sigproc(fn, data, hdr)
         fns.append(fn)
@@ -227,8 +228,77 @@ def test_dispatch_two_ranks_on_gpu(e2e):
     assert_peaks_equal(peaks, e2e["pipeline"]["peaks"])
 
 
+def _files_worker(rank, world, port, fns, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from riptide_amd.dispatch import search_files
+        from riptide_amd.worker_pool import GpuWorkerPool
+        c = inputs.CFG5
+        pool = GpuWorkerPool(c["dereddening"], c["ranges"], fmt="sigproc", batch=2, device=0)
+        peaks = search_files(fns, pool, chunksize=2)       # 4 files per rank: two chunks, prefetched
+        q.put((rank, [tuple(p) for p in peaks]))
+    except Exception as e:  # reported to the parent
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_search_files_two_ranks_cfg5(e2e, tmp_path):
+    """The multi-rank file path (dispatch.search_files: round-robin shard,
+    GpuWorkerPool.search_chunks with its prefetching page-locked ring, one
+    gather) over 2 gloo ranks driving cuda:0: the cfg5 files' peak lists
+    equal the reference's, in file order, on both ranks."""
+    import torch.multiprocessing as mp
+    fns = _cfg5_files(tmp_path, e2e)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_files_worker, args=(r, 2, port, fns, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=200) for _ in procs)
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert not isinstance(results[0], str), results[0]
+    assert not isinstance(results[1], str), results[1]
+    assert results[0] == results[1]
+    ref = _cfg5_golden_rows(e2e)
+    got = results[0]
+    assert [(p[7], p[5], p[4]) for p in got] == [r[:3] for r in ref]     # (dm, ip, iw)
+    s = np.array([p[6] for p in got])
+    r = np.array([x[3] for x in ref])
+    assert np.all(np.abs(s - r) <= 1e-4 * np.maximum(np.abs(r), 1.0))
+
+
+def test_worker_pool_mixed_shapes_matches_per_file(e2e, tmp_path):
+    """One chunk mixing two series lengths and an 8-bit file, with a device
+    batch that divides neither group: GpuWorkerPool groups by (length,
+    tsamp), splits into batches and returns the peaks in input order, equal
+    to searching every file on its own."""
+    from riptide_amd.reading import write_sigproc
+    from riptide_amd.worker_pool import GpuWorkerPool
+    c = inputs.CFG5
+    fns = []
+    for j, k in enumerate((0, 2, 7, 3, 4, 6, 1)):
+        n = (1 << 20) if j % 3 == 1 else (3 << 19)     # two lengths: 1 Mi and 1.5 Mi samples
+        data, hdr = inputs.cfg5_trial(k, n=n)
+        fn = str(tmp_path / f"mix_{j}.tim")
+        write_sigproc(fn, data, hdr)
+        fns.append(fn)
+    pool = GpuWorkerPool(c["dereddening"], c["ranges"][:2], fmt="sigproc", batch=3)
+    got = pool.process_fname_list(fns)
+    one = GpuWorkerPool(c["dereddening"], c["ranges"][:2], fmt="sigproc", batch=1)
+    ref = [p for fn in fns for p in one.process_fname(fn)]
+    assert len(got) == len(ref) > 0
+    assert [(p.dm, p.ip, p.iw) for p in got] == [(p.dm, p.ip, p.iw) for p in ref]
+    assert [p.snr for p in got] == [p.snr for p in ref]          # same kernels: identical
+
+
 # ---------------------------------------------------------------- C ABI robustness
-def test_plan_device_error_flag(monkeypatch):
+def test_plan_device_error_flag():
     """A unit that breaks its budget is refused by the kernel, which raises
     the plan's sticky flag; PeriodogramPlan.check / run(check=True) and the
     host-buffer periodogram raise instead of returning unwritten rows."""
@@ -239,15 +309,18 @@ def test_plan_device_error_flag(monkeypatch):
     args = (case["n"], case["tsamp"], case["pmin"], case["pmax"], case["bmin"], case["bmax"])
     good = engine.PeriodogramPlan.for_search(*args, ducy_max=case["ducy_max"])
     good.run(x, check=True)                                # no error on a valid plan
-    monkeypatch.setenv("RIPTIDE_AMD_DEBUG_CORRUPT_UNIT", "1")
-    bad = engine.PeriodogramPlan.for_search(*args, ducy_max=case["ducy_max"])
-    with pytest.raises(_lib.EngineError, match="LDS budget"):
-        bad.run(x, check=True)
-    bad.check()                                           # the flag was cleared by the failed check
-    with pytest.raises(_lib.EngineError, match="LDS budget"):
-        libcpp.periodogram(inputs.pgram_input(case), case["tsamp"], good.widths, case["pmin"], case["pmax"],
-                           case["bmin"], case["bmax"])
-    monkeypatch.delenv("RIPTIDE_AMD_DEBUG_CORRUPT_UNIT")
+    lib = _lib.load()
+    lib.rt_test_corrupt_next_plans(1)                      # test-only C entry point
+    try:
+        bad = engine.PeriodogramPlan.for_search(*args, ducy_max=case["ducy_max"])
+        with pytest.raises(_lib.EngineError, match="LDS budget"):
+            bad.run(x, check=True)
+        bad.check()                                       # the flag was cleared by the failed check
+        with pytest.raises(_lib.EngineError, match="LDS budget"):
+            libcpp.periodogram(inputs.pgram_input(case), case["tsamp"], good.widths, case["pmin"], case["pmax"],
+                               case["bmin"], case["bmax"])
+    finally:
+        lib.rt_test_corrupt_next_plans(0)
     good.check()
 
 

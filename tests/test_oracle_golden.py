@@ -132,3 +132,23 @@ def test_search_pipeline(oracle, golden, case):
     assert sha(periods) == str(golden[f"search_{name}_periods_sha"])
     ok, msg = snr_close(snrs, golden[f"search_{name}_snrs"])
     assert ok, msg
+
+
+# ---------------------------------------------------------------- input generators (CPU)
+# The full-size GPU parity tests regenerate their inputs on the box and fail
+# (not skip) when a generator drifts; these pin the same sha256s on the CPU, so
+# a numpy/libm change shows up in the CPU suite first.
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3", "cfg4"])
+def test_full_input_generators_pinned(golden_full, name):
+    g = golden_full["configs"][name]
+    assert sha(inputs.full_input(g["case"])) == g["input_sha"]
+
+
+def test_cfg5_input_generator_pinned():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden_e2e.json")) as f:
+        e2e = json.load(f)
+    for f in e2e["cfg5"]["files"][:3]:
+        data, _ = inputs.cfg5_trial(f["k"])
+        assert sha(data) == f["input_sha"], f"cfg5 trial {f['k']}"
