@@ -95,10 +95,26 @@ def cpu_baseline(workload="cfg2", cores="", extra=(), timeout_s=400):
 
 def cpu_baselines(workload, extra=()):
     """The rffa CPU model on this host: `cpu_baseline` on this process's CPU
-    share (16 cores per GPU on the GPU box), plus `node` on every affinity
-    core (the node-level comparison), each with its core count."""
+    share (16 cores per GPU on the GPU box), plus `node` on every core this
+    process may use (affinity mask capped by a cgroup CPU quota), each with
+    its core count.  Where the host grants fewer cores than its affinity mask
+    shows (a shared GPU box), `node_extrapolated` scales the measured
+    per-core rate to the affinity cores -- labelled, not measured."""
     share = cpu_baseline(workload, extra=extra)
-    share["node"] = cpu_baseline(workload, cores="all", extra=extra)
+    aff = share.get("affinity_cores")
+    quota = share.get("cpu_quota_cores")
+    usable = min(aff, int(quota)) if (aff and quota) else aff
+    if share.get("cores") and usable and usable > share["cores"]:
+        share["node"] = cpu_baseline(workload, cores="all", extra=extra)
+    else:
+        share["node"] = {"same_as_share": True, "cores": share.get("cores")}
+    node_cores = share["node"].get("cores") or 0
+    if aff and share.get("per_core_search_per_s") and node_cores < aff:
+        share["node_extrapolated"] = {
+            "value": share["per_core_search_per_s"] * aff, "unit": "DM trials/s", "cores": aff,
+            "basis": f"per-core rate of the {share.get('cores')}-core run x {aff} affinity cores; this host "
+                     f"grants {quota if quota else node_cores} cores, so the node figure is extrapolated, "
+                     f"not measured"}
     return share
 
 

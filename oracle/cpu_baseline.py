@@ -18,9 +18,10 @@ Workloads (bench.py legs):
         example.yaml range (periodogram + find_peaks).
 
 C = the worker processes used: `--cores N`, `--cores all` (every core of
-sched_getaffinity -- the node-level comparison), or by default this process's
-CPU share (sched_getaffinity capped by OMP_NUM_THREADS where the harness sets
-it: 16 host cores per GPU on the GPU box).  Workers are also capped so their
+sched_getaffinity that a cgroup CPU quota lets this process use -- the
+node-level comparison on a dedicated host), or by default this process's CPU
+share (sched_getaffinity capped by OMP_NUM_THREADS where the harness sets it,
+and by the CPU quota: 16 host cores per GPU on the GPU box).  Workers are also capped so their
 resident memory (measured ~0.5 GB per cfg2 trial) stays within half of the
 available memory and 120 GB.  Reports the search-only rate (deredden + normalise +
 periodogram: the work bench.py's GPU step does) as `value`, and search +
@@ -129,12 +130,38 @@ def _file(k):
     return t0, t1 - peaks, t1
 
 
+def cpu_quota():
+    """Cores' worth of CPU time this process's cgroup may use (cgroup v2
+    cpu.max or v1 cfs quota), or None when unlimited / unknown.  A shared
+    GPU box shows every core in the affinity mask but grants a share."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            return float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        if q > 0:
+            return q / per
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def default_cores():
     c = len(os.sched_getaffinity(0))
     for var in ("OMP_NUM_THREADS",):
         v = os.environ.get(var)
         if v and v.isdigit() and int(v) > 0:
             c = min(c, int(v))
+    q = cpu_quota()
+    if q:
+        c = min(c, max(1, int(q)))
     return c
 
 
@@ -159,8 +186,12 @@ def main():
     ap.add_argument("--files-from", default="", help="cfg5: text file with one SIGPROC path per line")
     _A = ap.parse_args()
     affinity = len(os.sched_getaffinity(0))
+    quota = cpu_quota()
     if _A.cores == "all":
-        cores = affinity
+        # every core this process may really use: the affinity mask, capped
+        # by a cgroup CPU quota (running more workers than the quota only
+        # time-slices them)
+        cores = min(affinity, max(1, int(quota))) if quota else affinity
     elif _A.cores:
         cores = int(_A.cores)
     else:
@@ -197,7 +228,9 @@ def main():
         "sample": f"{ntrials} {unit}, multiprocessing.Pool({cores}) one trial per process (rffa worker-pool "
                   f"model): numpy deredden+normalise + {what} periodogram = value; + find_peaks = "
                   f"search_and_peaks_per_s; {affinity} affinity cores on this host"
+                  + (f", cgroup CPU quota {quota:g} cores" if quota else "")
                   + (f", workers capped at {mem_cap} by available memory" if mem_cap and mem_cap < affinity else ""),
+        "affinity_cores": affinity, "cpu_quota_cores": quota,
         "seconds": total_wall}))
 
 

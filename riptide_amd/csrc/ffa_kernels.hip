@@ -1460,14 +1460,19 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
     const int lane = tid & 63;
     const int p = U.p;
     const int g = lane & (G - 1);
-    int j0 = min(g * c, p);
-    int cnt = min(j0 + c, p) - j0;                // columns of this lane (may be 0)
-    const int owner = (p - 1) / c;
     // rows with room for the wrapped prefix extension (final-pass output
     // levels at the S/N stride); only the register-window path uses it
     const bool ext = CH <= kSnrMaxChunk && q >= p + kSnrWin;
     // rows with room past p for a lane's whole CH-column prefix write
     const bool wfull = q >= p + CH;
+    // lanes past the row keep their natural chunk start g * c (their
+    // columns are masked) where the row stride holds every lane's chunk:
+    // clamped to p they read the banks of another row's lane (a 2-way
+    // conflict on every chunk and window read at p = 240-254)
+    const bool natural = ext && wfull && (G - 1) * c + CH <= q;
+    int j0 = natural ? g * c : min(g * c, p);
+    int cnt = max(min(j0 + c, p) - j0, 0);        // columns of this lane (may be 0)
+    const int owner = (p - 1) / c;
     constexpr int kRowsPerSet = kConeBlock / G;
     constexpr int rows_per_pass = NR * kRowsPerSet;
     constexpr int writer = G - 1;
@@ -1562,7 +1567,9 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
                     }
                 }
             } else {
-                const lds_ptr dummy = (lds_ptr)(data + kLdsDataFloats + 4);
+                // one dummy word per lane and column (the same word for
+                // every lane serialised those stores on one bank)
+                const lds_ptr dummy = (lds_ptr)(data + kLdsDataFloats + 4 + lane);
 #pragma unroll
                 for (int k = 0; k < NR; ++k) {
                     int cw = active[k] ? cnt : 0;
@@ -1876,6 +1883,9 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
 // CU's other workgroup filling the wait; two buffers (one workgroup per CU):
 // while unit u is merged in one, unit u + gridDim.x streams into the other.
 //   begin(u) [DMA] | wait | merge(u) | store or S/N(u)
+#ifndef RT_PRIO_HALF
+#define RT_PRIO_HALF 0
+#endif
 template <int SMAX, int RWT = 0>
 __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(ConeArgs a)
 {
@@ -1886,6 +1896,12 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
     __shared__ float whb[2 * kMaxWidths];   // S/N: h + b and b per width
 
     const int tid = threadIdx.x;
+#if RT_PRIO_HALF
+    // static priority for the second-dispatched half (waves 4-7, each
+    // sharing a SIMD with one of waves 0-3): MI355X_MICROARCH.md, two waves
+    // per SIMD, item 4
+    if (tid >= kConeBlock / 2) __builtin_amdgcn_s_setprio(1);
+#endif
 #ifdef RT_STAMPS
     const unsigned long long t_entry = __builtin_amdgcn_s_memtime();
     unsigned long long t_begin[3] = {};
