@@ -714,19 +714,13 @@ __device__ __forceinline__ void write_rows(float* base, float* dummy, const floa
 // lane 63 from lane 0 of the next slot, and bin p - 1 from bin 0.  Half the
 // LDS reads of the pair.
 //
-// Per-row terms of the row whose resolved descriptor sits in lane i.
+// Per-row terms from the row's scalars (SGPRs): r0 head row offset, r1..r3
+// the rolled rows' offsets (+ their rolls), t1..t3 the rolls, c1 carried.
 template <int SMAX, bool TWO>
-__device__ __forceinline__ void row_terms(lds_cptr l1, int p, int lane, int i, int o0, int o1, int o2, int o3, int s1,
-                                          int s2, int s3, float (&hs)[SMAX], float (&ts)[SMAX])
+__device__ __forceinline__ void row_terms_s(lds_cptr l1, int p, int lane, int r0, int r1, int r2, int r3, int t1,
+                                            int t2, int t3, int c1, float (&hs)[SMAX], float (&ts)[SMAX])
 {
-    // all of the row's scalars first, in distinct SGPRs: a v_readlane result
-    // read by the next VALU instruction costs s_nop wait states
     if constexpr (TWO) {
-        int r0 = __builtin_amdgcn_readlane(o0, i), r1 = __builtin_amdgcn_readlane(o1, i);
-        int r2 = __builtin_amdgcn_readlane(o2, i), r3 = __builtin_amdgcn_readlane(o3, i);
-        int t1 = __builtin_amdgcn_readlane(s1, i), t2 = __builtin_amdgcn_readlane(s2, i);
-        int t3 = __builtin_amdgcn_readlane(s3, i);
-        asm volatile("" : "+s"(r0), "+s"(r1), "+s"(r2), "+s"(r3), "+s"(t1), "+s"(t2), "+s"(t3));
         const lds_cptr hrow = l1 + r0;
         lds_cptr b1 = l1 + r1;
         lds_cptr b2 = l1 + r2;
@@ -746,11 +740,8 @@ __device__ __forceinline__ void row_terms(lds_cptr l1, int p, int lane, int i, i
             ts[k] = __fadd_rn(x2, x3);
         }
     } else {
-        // o0 head row, o1 tail row + shift, s1 shift, o2 carried (size-1 node:
+        // r0 head row, r1 tail row + shift, t1 shift, c1 carried (size-1 node:
         // the tail term is -0.0, x + (-0.0) == x exactly)
-        int r0 = __builtin_amdgcn_readlane(o0, i), r1 = __builtin_amdgcn_readlane(o1, i);
-        int t1 = __builtin_amdgcn_readlane(s1, i), c1 = __builtin_amdgcn_readlane(o2, i);
-        asm volatile("" : "+s"(r0), "+s"(r1), "+s"(t1), "+s"(c1));
         const lds_cptr hrow = l1 + r0;
         lds_cptr ta = l1 + r1;
         lds_cptr tw = ta - p;
@@ -764,6 +755,58 @@ __device__ __forceinline__ void row_terms(lds_cptr l1, int p, int lane, int i, i
             hs[k] = lds_ld(hrow + 64 * k);
             ts[k] = __uint_as_float((__float_as_uint(x) & keep) | neg0);
         }
+    }
+}
+
+// Per-row terms of the row whose resolved descriptor sits in lane i
+// (unpacked per lane: o0 .. o3, s1 .. s3; seven v_readlane per row).
+template <int SMAX, bool TWO>
+__device__ __forceinline__ void row_terms(lds_cptr l1, int p, int lane, int i, int o0, int o1, int o2, int o3, int s1,
+                                          int s2, int s3, float (&hs)[SMAX], float (&ts)[SMAX])
+{
+    // all of the row's scalars first, in distinct SGPRs: a v_readlane result
+    // read by the next VALU instruction costs s_nop wait states
+    if constexpr (TWO) {
+        int r0 = __builtin_amdgcn_readlane(o0, i), r1 = __builtin_amdgcn_readlane(o1, i);
+        int r2 = __builtin_amdgcn_readlane(o2, i), r3 = __builtin_amdgcn_readlane(o3, i);
+        int t1 = __builtin_amdgcn_readlane(s1, i), t2 = __builtin_amdgcn_readlane(s2, i);
+        int t3 = __builtin_amdgcn_readlane(s3, i);
+        asm volatile("" : "+s"(r0), "+s"(r1), "+s"(r2), "+s"(r3), "+s"(t1), "+s"(t2), "+s"(t3));
+        row_terms_s<SMAX, true>(l1, p, lane, r0, r1, r2, r3, t1, t2, t3, 0, hs, ts);
+    } else {
+        int r0 = __builtin_amdgcn_readlane(o0, i), r1 = __builtin_amdgcn_readlane(o1, i);
+        int t1 = __builtin_amdgcn_readlane(s1, i), c1 = __builtin_amdgcn_readlane(o2, i);
+        asm volatile("" : "+s"(r0), "+s"(r1), "+s"(t1), "+s"(c1));
+        row_terms_s<SMAX, false>(l1, p, lane, r0, r1, 0, 0, t1, 0, 0, c1, hs, ts);
+    }
+}
+
+// The same from a lane's packed 16-byte resolved entry (e.x: head row | first
+// rolled row << 16, e.y: the other two rolled rows, e.z: the three rolls,
+// carried bit 30): three v_readlane per row, the unpacking in scalar code.
+// A/B knob, off: same box, cone ms per cfg2 trial 7.97 / 7.95 with it vs
+// 7.61 / 7.64 without (the scalar unpacking costs more than the four
+// v_readlane it saves).
+#ifndef RT_PACKED_READLANE
+#define RT_PACKED_READLANE 0
+#endif
+template <int SMAX, bool TWO>
+__device__ __forceinline__ void row_terms_packed(lds_cptr l1, int p, int lane, int i, uint32_t ex, uint32_t ey,
+                                                 uint32_t ez, float (&hs)[SMAX], float (&ts)[SMAX])
+{
+    uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)ex, i);
+    uint32_t z = (uint32_t)__builtin_amdgcn_readlane((int)ez, i);
+    if constexpr (TWO) {
+        uint32_t y = (uint32_t)__builtin_amdgcn_readlane((int)ey, i);
+        asm volatile("" : "+s"(x), "+s"(y), "+s"(z));
+        const int t1 = (int)(z & 1023u), t2 = (int)((z >> 10) & 1023u), t3 = (int)((z >> 20) & 1023u);
+        row_terms_s<SMAX, true>(l1, p, lane, (int)(x & 0xFFFFu), (int)(x >> 16) + t1, (int)(y & 0xFFFFu) + t2,
+                                (int)(y >> 16) + t3, t1, t2, t3, 0, hs, ts);
+    } else {
+        asm volatile("" : "+s"(x), "+s"(z));
+        const int t1 = (int)(z & 1023u);
+        row_terms_s<SMAX, false>(l1, p, lane, (int)(x & 0xFFFFu), (int)(x >> 16) + t1, 0, 0, t1, 0, 0,
+                                 (int)((z >> 30) & 1u), hs, ts);
     }
 }
 
@@ -783,6 +826,7 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
     // lane i < 32 resolves row A of the wave's slot i, lane 32 + i its row B
     const int qi = lane & 31;
     int o0 = 0, o1 = 0, o2 = 0, o3 = 0, s1 = 0, s2 = 0, s3 = 0;
+    uint32_t ex = 0, ey = 0, ez = 0;      // the packed entry (RT_PACKED_READLANE)
     if constexpr (resolved_slots(SMAX)) {
         // host-resolved rows: one 16-byte entry per lane (the slot's row A in
         // lanes 0-31 with the slot word, row B in lanes 32-63)
@@ -791,6 +835,9 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
         const int qc = qi < Q ? qi : Q - 1;
         const uint4 e = reinterpret_cast<const uint4*>(st)[1 + (lane >> 5) * (kConeWaves * Q) + wave * Q + qc];
         sw = lane < 32 ? e.w : 0u;
+        ex = e.x;
+        ey = e.y;
+        ez = e.z;
         s1 = (int)(e.z & 1023u);
         if constexpr (TWO) {
             s2 = (int)((e.z >> 10) & 1023u);
@@ -846,7 +893,10 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
         if (q < nq) {
             const uint32_t kq = (uint32_t)__builtin_amdgcn_readlane((int)sw, q) >> 20;
             float hs[SMAX], ts[SMAX];
-            row_terms<SMAX, TWO>(l1, p, lane, q, o0, o1, o2, o3, s1, s2, s3, hs, ts);
+            if constexpr (resolved_slots(SMAX) && RT_PACKED_READLANE)
+                row_terms_packed<SMAX, TWO>(l1, p, lane, q, ex, ey, ez, hs, ts);
+            else
+                row_terms<SMAX, TWO>(l1, p, lane, q, o0, o1, o2, o3, s1, s2, s3, hs, ts);
 #pragma unroll
             for (int k = 0; k < SMAX; ++k) v[2 * q][k] = __fadd_rn(hs[k], ts[k]);
             const int qb = 2 * q + 1 < RW ? 2 * q + 1 : RW - 1;   // row B's register row (q < Q: in range)
@@ -863,7 +913,10 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
                         v[qb][k] = __fadd_rn(hs[k], x);
                     }
                 } else if (kq == kSlotTwo) {
-                    row_terms<SMAX, TWO>(l1, p, lane, 32 + q, o0, o1, o2, o3, s1, s2, s3, hs, ts);
+                    if constexpr (resolved_slots(SMAX) && RT_PACKED_READLANE)
+                        row_terms_packed<SMAX, TWO>(l1, p, lane, 32 + q, ex, ey, ez, hs, ts);
+                    else
+                        row_terms<SMAX, TWO>(l1, p, lane, 32 + q, o0, o1, o2, o3, s1, s2, s3, hs, ts);
 #pragma unroll
                     for (int k = 0; k < SMAX; ++k) v[qb][k] = __fadd_rn(hs[k], ts[k]);
                 }
@@ -978,10 +1031,11 @@ __device__ __forceinline__ void merge_step_lanes(const UnitCtx& C, const float* 
             const int o1 = FIRST ? loff[q1] : (int)__umul24(q1, (uint32_t)p);
             const int o2 = FIRST ? loff[q2] : (int)__umul24(q2, (uint32_t)p);
             const int o3 = FIRST ? loff[q3] : (int)__umul24(q3, (uint32_t)p);
-            int i1 = j + sH, i2 = j + sh, i3 = j + sTT;
-            i1 = i1 >= p ? i1 - p : i1;
-            i2 = i2 >= p ? i2 - p : i2;
-            i3 = i3 >= p ? i3 - p : i3;
+            // (j + s) mod p for j, s < p: min of the sum and the sum - p as
+            // unsigned (the latter wraps to a huge value below p)
+            uint32_t u1 = (uint32_t)(j + sH), u2 = (uint32_t)(j + sh), u3 = (uint32_t)(j + sTT);
+            const int i1 = (int)min(u1, u1 - (uint32_t)p), i2 = (int)min(u2, u2 - (uint32_t)p);
+            const int i3 = (int)min(u3, u3 - (uint32_t)p);
             const float x0 = lds_ld(sp + o0 + j);
             const float x1 = lds_ld(sp + o1 + i1);
             const float x2 = lds_ld(sp + o2 + i2);
@@ -994,8 +1048,8 @@ __device__ __forceinline__ void merge_step_lanes(const UnitCtx& C, const float* 
             const int sh = (int)(d >> 20);
             const int ho = FIRST ? loff[d & 1023u] : (int)__umul24(d & 1023u, (uint32_t)p);
             const int to = car ? ho : (FIRST ? loff[tc & 1023u] : (int)__umul24(tc, (uint32_t)p));
-            int i1 = j + sh;
-            i1 = i1 >= p ? i1 - p : i1;
+            const uint32_t u1 = (uint32_t)(j + sh);
+            const int i1 = (int)min(u1, u1 - (uint32_t)p);
             const float x0 = lds_ld(sp + ho + j);
             float x1 = lds_ld(sp + to + i1);
             x1 = car ? -0.0f : x1;
@@ -1391,6 +1445,69 @@ __device__ __forceinline__ void window_dispatch2(int w, const float (&z0)[CH + k
     }
 }
 
+// The standard ladder of small boxcar widths: generate_width_trials
+// (ffautils.py:3-10) with wtsp 1.5 always starts 1, 2, 3, 4, 6, 9 (every
+// BASELINE config: W = 6 or 10 from 240 bins).  When a plan's widths begin
+// with it, the S/N evaluates those six window maxima in one straight block
+// (independent v_max3 chains the compiler may interleave, no width switch,
+// one interleaved DPP all-reduce), instead of one switch case and one
+// all-reduce per width.  Same float operations, same results.
+#ifndef RT_SNR_STD6
+#define RT_SNR_STD6 1
+#endif
+constexpr int kStdWidths[6] = {1, 2, 3, 4, 6, 9};
+
+template <int CH, int W>
+__device__ __forceinline__ float window_max_nv(const float (&z)[CH + kSnrWin], const float (&cp)[CH])
+{
+    // diff_max (kernels.hpp:50-60) as window_max, without volatile: the six
+    // widths' chains are independent and may be interleaved
+    float dm = -INFINITY;
+#pragma unroll
+    for (int i = 0; i + 1 < CH; i += 2) {
+        float t0, t1;
+        asm("v_sub_f32 %1, %3, %4\n\tv_sub_f32 %2, %5, %6\n\tv_max3_f32 %0, %0, %1, %2"
+            : "+v"(dm), "=&v"(t0), "=&v"(t1)
+            : "v"(z[i + W]), "v"(cp[i]), "v"(z[i + 1 + W]), "v"(cp[i + 1]));
+    }
+    if constexpr (CH & 1) {
+        float t0;
+        asm("v_sub_f32 %1, %2, %3\n\tv_max_f32 %0, %0, %1" : "+v"(dm), "=&v"(t0) : "v"(z[CH - 1 + W]), "v"(cp[CH - 1]));
+    }
+    return dm;
+}
+
+// one v_max_f32 with a DPP source per value and step, six values interleaved
+// (each DPP reads a register written six instructions earlier: no wait states)
+#define RT_MAX6_STEP(CTRL)                                                                                  \
+    asm volatile("v_max_f32_dpp %0, %0, %0 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                        \
+                 "v_max_f32_dpp %1, %1, %1 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                        \
+                 "v_max_f32_dpp %2, %2, %2 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                        \
+                 "v_max_f32_dpp %3, %3, %3 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                        \
+                 "v_max_f32_dpp %4, %4, %4 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                        \
+                 "v_max_f32_dpp %5, %5, %5 " CTRL " row_mask:0xf bank_mask:0xf"                              \
+                 : "+v"(m[0]), "+v"(m[1]), "+v"(m[2]), "+v"(m[3]), "+v"(m[4]), "+v"(m[5]))
+
+// The six standard widths' row maxima all-reduced over each G-lane group
+// (grp_allmax for six values at once); lane g of a group then keeps width g.
+template <int CH, int G>
+__device__ __forceinline__ float snr_std6(const float (&z)[CH + kSnrWin], const float (&cp)[CH], int g)
+{
+    static_assert(G == 8 || G == 16, "one DPP row per group");
+    float m[6] = {window_max_nv<CH, 1>(z, cp), window_max_nv<CH, 2>(z, cp), window_max_nv<CH, 3>(z, cp),
+                  window_max_nv<CH, 4>(z, cp), window_max_nv<CH, 6>(z, cp), window_max_nv<CH, 9>(z, cp)};
+    asm volatile("s_nop 1" ::: "memory");
+    RT_MAX6_STEP("quad_perm:[1,0,3,2]");
+    RT_MAX6_STEP("quad_perm:[2,3,0,1]");
+    RT_MAX6_STEP("row_half_mirror");
+    if constexpr (G >= 16) RT_MAX6_STEP("row_mirror");
+    float r = m[0];
+#pragma unroll
+    for (int i = 1; i < 6; ++i) r = g == i ? m[i] : r;
+    return r;
+}
+#undef RT_MAX6_STEP
+
 #ifdef RT_STAMPS
 #define RT_SNR_MARK(i)                                                           \
     do {                                                                         \
@@ -1482,6 +1599,10 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
     // the widths in lanes (lane i: width i), taken per width by v_readlane
     // instead of an LDS read and its wait
     const int wlane = wl[min(lane, (int)nw - 1)];
+    // the plan's widths begin with the standard ladder 1, 2, 3, 4, 6, 9
+    bool std6 = nw >= 6;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) std6 = std6 && __builtin_amdgcn_readlane(wlane, i) == kStdWidths[i];
     for (int base = 0; base < nev; base += rows_per_pass) {
         // opaque per row pass: the column masks (i < cnt, j0 + k >= p) are
         // recomputed by one v_cmp each instead of being hoisted out of the
@@ -1688,10 +1809,18 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
                 }
             }
             RT_SNR_MARK(9);
+            uint32_t iw0 = 0;
+            if constexpr (RT_SNR_STD6 && NR == 1 && kSnrTransEmit && (G == 8 || G == 16)) {
+                if (std6) {
+                    // widths 0-5 are the standard ladder: lane g < 6 keeps width g
+                    sel[0][0] = snr_std6<CH, G>(z[0], cp[0], g);
+                    iw0 = 6;
+                }
+            }
 #ifdef RT_DIAG_SNR_WIDTHS
-            for (uint32_t iw = 0; iw < min(nw, (uint32_t)RT_DIAG_SNR_WIDTHS); ++iw) {   // diagnostics only (wrong results)
+            for (uint32_t iw = iw0; iw < min(nw, (uint32_t)RT_DIAG_SNR_WIDTHS); ++iw) {   // diagnostics only (wrong results)
 #else
-            for (uint32_t iw = 0; iw < nw; ++iw) {
+            for (uint32_t iw = iw0; iw < nw; ++iw) {
 #endif
                 const int w = __builtin_amdgcn_readlane(wlane, (int)iw);
                 if (w <= kSnrWin) {
