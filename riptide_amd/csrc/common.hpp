@@ -83,7 +83,15 @@ enum : int {
 // r, r + 1 with the same head and tail rows and roll shifts s, s + 1 (the
 // second row's tail term is the first's shifted by one bin).  Slot word:
 // row A | row B << 10 | kind << 20.
-enum : uint32_t { kSlotOne = 0, kSlotTwo = 1, kSlotPair = 2 };
+enum : uint32_t { kSlotOne = 0, kSlotTwo = 1, kSlotPair = 2, kSlotHalf = 3 };
+// kSlotHalf: rows r, r + 1 with the same head row (not a pair: their tails or
+// shifts differ -- an odd-sized node's consecutive outputs), so the head term
+// (the level-l+1 head row H', or H for a single step) is computed once for
+// both and only row B's tail term is read (RT_SLOT_HALF: the planner emits
+// them; the kernel always runs them)
+#ifndef RT_SLOT_HALF
+#define RT_SLOT_HALF 1
+#endif
 constexpr int kSlotWords = kConeWgsPerCu == 4 ? 288 : 544;   // LDS area of a unit's slot tables
 // 4/5-slot variants (p = 193-320, rows <= 72 per unit): slot tables with
 // every row resolved (build_tile_blob), 16 bytes per row: source-row LDS

@@ -716,11 +716,26 @@ __device__ __forceinline__ void write_rows(float* base, float* dummy, const floa
 //
 // Per-row terms from the row's scalars (SGPRs): r0 head row offset, r1..r3
 // the rolled rows' offsets (+ their rolls), t1..t3 the rolls, c1 carried.
-template <int SMAX, bool TWO>
+// HEAD false (row B of a kSlotHalf): only the tail term; hs is row A's.
+template <int SMAX, bool TWO, bool HEAD = true>
 __device__ __forceinline__ void row_terms_s(lds_cptr l1, int p, int lane, int r0, int r1, int r2, int r3, int t1,
                                             int t2, int t3, int c1, float (&hs)[SMAX], float (&ts)[SMAX])
 {
-    if constexpr (TWO) {
+    if constexpr (TWO && !HEAD) {
+        lds_cptr b2 = l1 + r2;
+        lds_cptr b3 = l1 + r3;
+        lds_cptr w2 = b2 - p, w3 = b3 - p;
+        asm("" : "+v"(b2), "+v"(w2), "+v"(b3), "+v"(w3));
+        const int ls2 = lane + t2;
+        const int ls3 = lane + t3;
+#pragma unroll
+        for (int k = 0; k < SMAX; ++k) {
+            const int wk = p - 64 * k;
+            const float x2 = lds_ld((ls2 >= wk ? w2 : b2) + 64 * k);
+            const float x3 = lds_ld((ls3 >= wk ? w3 : b3) + 64 * k);
+            ts[k] = __fadd_rn(x2, x3);
+        }
+    } else if constexpr (TWO) {
         const lds_cptr hrow = l1 + r0;
         lds_cptr b1 = l1 + r1;
         lds_cptr b2 = l1 + r2;
@@ -739,6 +754,14 @@ __device__ __forceinline__ void row_terms_s(lds_cptr l1, int p, int lane, int r0
             hs[k] = __fadd_rn(lds_ld(hrow + 64 * k), x1);
             ts[k] = __fadd_rn(x2, x3);
         }
+    } else if constexpr (!HEAD) {
+        // single step, row B of a half: its tail only (never carried)
+        lds_cptr ta = l1 + r1;
+        lds_cptr tw = ta - p;
+        asm("" : "+v"(ta), "+v"(tw));
+        const int ls = lane + t1;
+#pragma unroll
+        for (int k = 0; k < SMAX; ++k) ts[k] = lds_ld((ls >= p - 64 * k ? tw : ta) + 64 * k);
     } else {
         // r0 head row, r1 tail row + shift, t1 shift, c1 carried (size-1 node:
         // the tail term is -0.0, x + (-0.0) == x exactly)
@@ -760,24 +783,37 @@ __device__ __forceinline__ void row_terms_s(lds_cptr l1, int p, int lane, int r0
 
 // Per-row terms of the row whose resolved descriptor sits in lane i
 // (unpacked per lane: o0 .. o3, s1 .. s3; seven v_readlane per row).
-template <int SMAX, bool TWO>
+template <int SMAX, bool TWO, bool HEAD = true>
 __device__ __forceinline__ void row_terms(lds_cptr l1, int p, int lane, int i, int o0, int o1, int o2, int o3, int s1,
                                           int s2, int s3, float (&hs)[SMAX], float (&ts)[SMAX])
 {
     // all of the row's scalars first, in distinct SGPRs: a v_readlane result
     // read by the next VALU instruction costs s_nop wait states
     if constexpr (TWO) {
-        int r0 = __builtin_amdgcn_readlane(o0, i), r1 = __builtin_amdgcn_readlane(o1, i);
-        int r2 = __builtin_amdgcn_readlane(o2, i), r3 = __builtin_amdgcn_readlane(o3, i);
-        int t1 = __builtin_amdgcn_readlane(s1, i), t2 = __builtin_amdgcn_readlane(s2, i);
-        int t3 = __builtin_amdgcn_readlane(s3, i);
-        asm volatile("" : "+s"(r0), "+s"(r1), "+s"(r2), "+s"(r3), "+s"(t1), "+s"(t2), "+s"(t3));
-        row_terms_s<SMAX, true>(l1, p, lane, r0, r1, r2, r3, t1, t2, t3, 0, hs, ts);
+        if constexpr (HEAD) {
+            int r0 = __builtin_amdgcn_readlane(o0, i), r1 = __builtin_amdgcn_readlane(o1, i);
+            int r2 = __builtin_amdgcn_readlane(o2, i), r3 = __builtin_amdgcn_readlane(o3, i);
+            int t1 = __builtin_amdgcn_readlane(s1, i), t2 = __builtin_amdgcn_readlane(s2, i);
+            int t3 = __builtin_amdgcn_readlane(s3, i);
+            asm volatile("" : "+s"(r0), "+s"(r1), "+s"(r2), "+s"(r3), "+s"(t1), "+s"(t2), "+s"(t3));
+            row_terms_s<SMAX, true>(l1, p, lane, r0, r1, r2, r3, t1, t2, t3, 0, hs, ts);
+        } else {
+            int r2 = __builtin_amdgcn_readlane(o2, i), r3 = __builtin_amdgcn_readlane(o3, i);
+            int t2 = __builtin_amdgcn_readlane(s2, i), t3 = __builtin_amdgcn_readlane(s3, i);
+            asm volatile("" : "+s"(r2), "+s"(r3), "+s"(t2), "+s"(t3));
+            row_terms_s<SMAX, true, false>(l1, p, lane, 0, 0, r2, r3, 0, t2, t3, 0, hs, ts);
+        }
     } else {
-        int r0 = __builtin_amdgcn_readlane(o0, i), r1 = __builtin_amdgcn_readlane(o1, i);
-        int t1 = __builtin_amdgcn_readlane(s1, i), c1 = __builtin_amdgcn_readlane(o2, i);
-        asm volatile("" : "+s"(r0), "+s"(r1), "+s"(t1), "+s"(c1));
-        row_terms_s<SMAX, false>(l1, p, lane, r0, r1, 0, 0, t1, 0, 0, c1, hs, ts);
+        if constexpr (HEAD) {
+            int r0 = __builtin_amdgcn_readlane(o0, i), r1 = __builtin_amdgcn_readlane(o1, i);
+            int t1 = __builtin_amdgcn_readlane(s1, i), c1 = __builtin_amdgcn_readlane(o2, i);
+            asm volatile("" : "+s"(r0), "+s"(r1), "+s"(t1), "+s"(c1));
+            row_terms_s<SMAX, false>(l1, p, lane, r0, r1, 0, 0, t1, 0, 0, c1, hs, ts);
+        } else {
+            int r1 = __builtin_amdgcn_readlane(o1, i), t1 = __builtin_amdgcn_readlane(s1, i);
+            asm volatile("" : "+s"(r1), "+s"(t1));
+            row_terms_s<SMAX, false, false>(l1, p, lane, 0, r1, 0, 0, t1, 0, 0, 0, hs, ts);
+        }
     }
 }
 
@@ -854,7 +890,7 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
         (void)loff;
     } else {
     sw = qi < nq ? st[1 + wave + kConeWaves * qi] : 0u;
-    const bool act = qi < nq && (lane < 32 || (sw >> 20) == kSlotTwo);
+    const bool act = qi < nq && (lane < 32 || (sw >> 20) == kSlotTwo || (sw >> 20) == kSlotHalf);
     const int r = lane < 32 ? (int)(sw & 1023u) : (int)((sw >> 10) & 1023u);
     const uint32_t* const desc = desc_table(C);
     // the first step reads the bottom level through its row offsets: a
@@ -912,6 +948,12 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
                         x = lane == (k + 1 < SMAX ? 63 : jl) ? __int_as_float(n0[k]) : x;
                         v[qb][k] = __fadd_rn(hs[k], x);
                     }
+                } else if (kq == kSlotHalf) {
+                    // row B shares row A's head term: only its tail term
+                    float tb[SMAX];
+                    row_terms<SMAX, TWO, false>(l1, p, lane, 32 + q, o0, o1, o2, o3, s1, s2, s3, hs, tb);
+#pragma unroll
+                    for (int k = 0; k < SMAX; ++k) v[qb][k] = __fadd_rn(hs[k], tb[k]);
                 } else if (kq == kSlotTwo) {
                     if constexpr (resolved_slots(SMAX) && RT_PACKED_READLANE)
                         row_terms_packed<SMAX, TWO>(l1, p, lane, 32 + q, ex, ey, ez, hs, ts);
@@ -928,14 +970,21 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
 // Slot-step write-back into the dense LDS rows at base / store to global
 // memory (a non-final pass's output level): register rows 2q, 2q + 1 to the
 // slot's rows A and B.
+// zpad (a final pass's output level at the S/N stride q): the bins past p
+// up to q are written as +0.0, so the S/N reads its chunks without masking
+// the columns past the row (adding +0.0 to its fp64 partial sums is exact).
 template <int SMAX, int RW>
 __device__ __forceinline__ void write_rows_slots(float* base, float* dummy, const float (&v)[RW][SMAX], int p,
-                                                 int lane, uint32_t sw, int nq, int q)
+                                                 int lane, uint32_t sw, int nq, int q, bool zpad = false)
 {
 #if RT_SLOT_OPAQUE_LANE
     asm volatile("" : "+v"(lane));
 #endif
     const bool tail_ok = lane + 64 * (SMAX - 1) < p;
+    // zpad: the last slot's lanes past p store +0.0 at their own bin (when it
+    // lies inside the stride), and lanes past 64 SMAX clear the rest of it
+    const bool tail_zero = zpad && !tail_ok && lane + 64 * (SMAX - 1) < q;
+    const bool rest_zero = zpad && lane + 64 * SMAX < q;
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
         if (i / 2 < nq) {
@@ -946,8 +995,9 @@ __device__ __forceinline__ void write_rows_slots(float* base, float* dummy, cons
 #pragma unroll
                 for (int k = 0; k < SMAX; ++k) {
                     if (k < SMAX - 1) orow[64 * k] = v[i][k];
-                    else *(tail_ok ? orow + 64 * k : dummy) = v[i][k];
+                    else *((tail_ok || tail_zero) ? orow + 64 * k : dummy) = tail_ok ? v[i][k] : 0.0f;
                 }
+                if (zpad && 64 * SMAX < q) *(rest_zero ? orow + 64 * SMAX : dummy) = 0.0f;
             }
         }
     }
@@ -1113,7 +1163,7 @@ __device__ __forceinline__ void store_rows_lanes(const float (&v)[RW][1], int p,
 template <int SMAX, int RW>
 __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int p, int L, int tid, bool st,
                                              __amdgpu_buffer_rsrc_t rs, uint32_t st_o0, uint32_t flags, float* dummy,
-                                             int qout)
+                                             int qout, bool zpad)
 {
     const int lane = tid & 63, wave = tid >> 6;
     const bool tile = C.tile;
@@ -1182,7 +1232,8 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
                 if (!(flags & kConeDiagNoBarrier)) lds_barrier();
                 // the output level of a final pass at row stride qout (the S/N's)
                 if (!(flags & kConeDiagNoWrite))
-                    write_rows_slots<SMAX, RW>(base, dummy, v, p, lane, sw, nq, lo == 0 ? qout : p);
+                    write_rows_slots<SMAX, RW>(base, dummy, v, p, lane, sw, nq, lo == 0 ? qout : p,
+                                               lo == 0 && zpad);
                 if (!(flags & kConeDiagNoBarrier)) lds_barrier();
             }
             return;
@@ -1572,7 +1623,8 @@ __device__ __forceinline__ float grp_allmax(float v)
 // row passes -- barriers, DPP scans -- per unit).
 template <int CH, int G, int NR = 1>
 __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, float* data, int q, const int* wl,
-                                         int nev, int c, int tid, const float* whb, unsigned long long* tl)
+                                         int nev, int c, int tid, const float* whb, unsigned long long* tl,
+                                         bool zpad = false)
 {
     const int lane = tid & 63;
     const int p = U.p;
@@ -1588,6 +1640,10 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
     // conflict on every chunk and window read at p = 240-254)
     const bool natural = ext && wfull && (G - 1) * c + CH <= q;
     int j0 = natural ? g * c : min(g * c, p);
+    // every column a lane reads lies in [0, q), the merge cleared [p, q),
+    // and each lane's chunk is exactly its CH registers (c < CH: the columns
+    // past the chunk are the next lane's and stay masked)
+    const bool unmasked = zpad && natural && c == CH;
     int cnt = max(min(j0 + c, p) - j0, 0);        // columns of this lane (may be 0)
     const int owner = (p - 1) / c;
     constexpr int kRowsPerSet = kConeBlock / G;
@@ -1620,17 +1676,25 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
             row[k] = data + min(r[k], nev - 1) * q + j0;
         }
         // every lane reads CH columns at immediate offsets (past its chunk:
-        // the next chunk, the next row or the LDS pad), masked to 0
+        // the next chunk, the next row or the LDS pad), masked to 0 -- or,
+        // zero-padded rows (the merge stored +0.0 past p), unmasked
+        if (unmasked) {
 #pragma unroll
-        for (int k = 0; k < NR; ++k)
+            for (int k = 0; k < NR; ++k)
 #pragma unroll
-            for (int i = 0; i < CH; ++i) {
-                const float x = row[k][i];
-                cp[k][i] = i < cnt ? x : 0.0f;
-                // the select on the float, before the fp64 conversion (else
-                // two selects on the converted halves)
-                asm("" : "+v"(cp[k][i]));
-            }
+                for (int i = 0; i < CH; ++i) cp[k][i] = row[k][i];
+        } else {
+#pragma unroll
+            for (int k = 0; k < NR; ++k)
+#pragma unroll
+                for (int i = 0; i < CH; ++i) {
+                    const float x = row[k][i];
+                    cp[k][i] = i < cnt ? x : 0.0f;
+                    // the select on the float, before the fp64 conversion (else
+                    // two selects on the converted halves)
+                    asm("" : "+v"(cp[k][i]));
+                }
+        }
         // fp64 prefix: the masked columns add +0.0 (the partial sums start at
         // +0.0 and are never -0.0, so the additions are exact no-ops)
 #pragma unroll
@@ -1899,7 +1963,7 @@ constexpr bool variant_has_group(int smax, int G)
 
 template <int SMAX>
 __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& U, float* data, int q, const int* wl,
-                                             int nrows, int tid, float* whb, unsigned long long* tl)
+                                             int nrows, int tid, float* whb, unsigned long long* tl, bool zpad = false)
 {
     const int lane = tid & 63, wave = tid >> 6;
     const int p = U.p;
@@ -1923,27 +1987,27 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
         // short rows (p <= 40 / 72): register chunks sized to the row, not 17
         if constexpr (variant_has_group(SMAX, 8)) {
             if (G == 8) {
-                if (c <= 5) snr_rows<5, 8>(a, U, data, q, wl, nev, c, tid, whb, tl);
-                else if (c <= 9) snr_rows<9, 8>(a, U, data, q, wl, nev, c, tid, whb, tl);
-                else snr_rows<kSnrMaxChunk, 8>(a, U, data, q, wl, nev, c, tid, whb, tl);
+                if (c <= 5) snr_rows<5, 8>(a, U, data, q, wl, nev, c, tid, whb, tl, zpad);
+                else if (c <= 9) snr_rows<9, 8>(a, U, data, q, wl, nev, c, tid, whb, tl, zpad);
+                else snr_rows<kSnrMaxChunk, 8>(a, U, data, q, wl, nev, c, tid, whb, tl, zpad);
                 return;
             }
         }
         if constexpr (variant_has_group(SMAX, 16)) {
             if (G == 16) {
-                snr_rows<kSnrMaxChunk, 16, RT_SNR_ROWS>(a, U, data, q, wl, nev, c, tid, whb, tl);
+                snr_rows<kSnrMaxChunk, 16, RT_SNR_ROWS>(a, U, data, q, wl, nev, c, tid, whb, tl, zpad);
                 return;
             }
         }
         if constexpr (variant_has_group(SMAX, 32)) {
             if (G == 32) {
-                snr_rows<kSnrMaxChunk, 32>(a, U, data, q, wl, nev, c, tid, whb, tl);
+                snr_rows<kSnrMaxChunk, 32>(a, U, data, q, wl, nev, c, tid, whb, tl, zpad);
                 return;
             }
         }
-        if constexpr (variant_has_group(SMAX, 64)) snr_rows<kSnrMaxChunk, 64>(a, U, data, q, wl, nev, c, tid, whb, tl);
+        if constexpr (variant_has_group(SMAX, 64)) snr_rows<kSnrMaxChunk, 64>(a, U, data, q, wl, nev, c, tid, whb, tl, zpad);
     } else if (c <= kSnrChunk) {
-        if constexpr (variant_has_group(SMAX, 64)) snr_rows<kSnrChunk, 64>(a, U, data, q, wl, nev, c, tid, whb, tl);
+        if constexpr (variant_has_group(SMAX, 64)) snr_rows<kSnrChunk, 64>(a, U, data, q, wl, nev, c, tid, whb, tl, zpad);
     } else if constexpr (variant_pmax(SMAX) > 64 * kSnrChunk) {
         // very wide rows (p > 64 * kSnrChunk): one wave per row, chunks from LDS
         const int g = lane;
@@ -2014,6 +2078,13 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
 //   begin(u) [DMA] | wait | merge(u) | store or S/N(u)
 #ifndef RT_PRIO_HALF
 #define RT_PRIO_HALF 0
+#endif
+// final-pass rows zero-padded past p for unmasked S/N chunk reads (A/B knob,
+// off: same box, cone ms per cfg2 trial 7.98 / 7.97 with it vs 7.86 / 7.81
+// without -- the merge's extra zero stores and the second S/N read path cost
+// more than the 17 column selects per row pass they save)
+#ifndef RT_SNR_ZPAD
+#define RT_SNR_ZPAD 0
 #endif
 template <int SMAX, int RWT = 0>
 __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(ConeArgs a)
@@ -2100,9 +2171,14 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
                 if (!st && L > 0 && C.slots && (a.flags & kConeFuse2) && (a.flags & kConeSnrStride))
                     qout = n0 * qa <= kLdsDataFloats ? qa : (n0 * qb <= kLdsDataFloats ? qb : p);
             }
+            // the S/N's chunks read without column masks (zero-padded rows):
+            // a final pass whose output level the row-slot write-back stores
+            // at the S/N stride with room for every lane's whole chunk
+            const bool zpad = RT_SNR_ZPAD && !st && L > 0 && C.slots && (a.flags & kConeFuse2) &&
+                              SMAX <= 5 && SMAX != kPack2 && qout >= p + kSnrMaxChunk;
             if (L > 0 && !(a.flags & kConeDiagNoMerge))
                 merge_levels<SMAX, RW>(C, buf, p, L, tid, st_regs, rs, o0, a.flags, buf + kLdsBufFloats + 4 + (tid & 63),
-                                       qout);
+                                       qout, zpad);
             RT_MARK(3);
             // the output level: dense rows from the buffer start, or (no merge
             // level) the single bottom row where the DMA left it
@@ -2116,9 +2192,9 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
                 }
             } else {
 #ifdef RT_STAMPS
-                if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX>(a, U, obase, qout, wl, n0, tid, whb, tl);
+                if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX>(a, U, obase, qout, wl, n0, tid, whb, tl, zpad);
 #else
-                if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX>(a, U, obase, qout, wl, n0, tid, whb, nullptr);
+                if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX>(a, U, obase, qout, wl, n0, tid, whb, nullptr, zpad);
 #endif
             }
         }

@@ -428,22 +428,27 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
 
 // Row slots of one merge step (output level with n rows, descriptors d):
 // rows in order, a pair where rows r, r + 1 share head and tail rows with
-// shifts s, s + 1 (never carried rows), filled into the slots g = wave + 8q
-// of the wave's register rows 2q, 2q + 1 (capacity 2, or 1 for the last
-// slot of an odd RW).  Every slot is filled to its capacity (a pair split
-// into two rows where needed), so n <= 8 RW rows always fit.
+// shifts s, s + 1 (never carried rows), else (RT_SLOT_HALF) a half where
+// they share only the head row (neither carried), filled into the slots
+// g = wave + 8q of the wave's register rows 2q, 2q + 1 (capacity 2, or 1 for
+// the last slot of an odd RW).  Every slot is filled to its capacity (a pair
+// or half split into two rows where needed), so n <= 8 RW rows always fit.
 static void build_row_slots(const uint32_t* d, uint32_t n, uint32_t p, int rw, std::vector<uint32_t>& slots)
 {
-    struct Item { uint32_t r; bool pair; };
+    struct Item { uint32_t r; uint32_t kind; };   // kSlotOne (a single row), kSlotPair or kSlotHalf
     std::vector<Item> items;
     for (uint32_t r = 0; r < n;) {
         const uint32_t a = d[r];
-        if (r + 1 < n && ((a ^ d[r + 1]) & 0xFFFFFu) == 0 && ((a >> 10) & 1023u) != kCarriedRow &&
-            (d[r + 1] >> 20) == ((a >> 20) + 1) % p) {
-            items.push_back({r, true});
+        const bool carried = ((a >> 10) & 1023u) == kCarriedRow;
+        if (r + 1 < n && ((a ^ d[r + 1]) & 0xFFFFFu) == 0 && !carried && (d[r + 1] >> 20) == ((a >> 20) + 1) % p) {
+            items.push_back({r, kSlotPair});
+            r += 2;
+        } else if (RT_SLOT_HALF && r + 1 < n && ((a ^ d[r + 1]) & 1023u) == 0 && !carried &&
+                   ((d[r + 1] >> 10) & 1023u) != kCarriedRow) {
+            items.push_back({r, kSlotHalf});
             r += 2;
         } else {
-            items.push_back({r, false});
+            items.push_back({r, kSlotOne});
             r += 1;
         }
     }
@@ -454,15 +459,15 @@ static void build_row_slots(const uint32_t* d, uint32_t n, uint32_t p, int rw, s
         if (g >= kConeWaves * Q) throw std::runtime_error("schedule: merge level exceeds the register rows");
         const int cap = (g / kConeWaves == Q - 1 && (rw & 1)) ? 1 : 2;
         Item& A = items[c];
-        if (A.pair && cap == 2) {
-            slots.push_back(A.r | ((A.r + 1) << 10) | (kSlotPair << 20));
+        if (A.kind != kSlotOne && cap == 2) {
+            slots.push_back(A.r | ((A.r + 1) << 10) | (A.kind << 20));
             ++c;
             continue;
         }
         const uint32_t ra = A.r;
-        if (A.pair) {            // split: row A alone, its partner stays next
+        if (A.kind != kSlotOne) {   // split: row A alone, its partner stays next
             A.r += 1;
-            A.pair = false;
+            A.kind = kSlotOne;
         } else {
             ++c;
         }
@@ -472,9 +477,9 @@ static void build_row_slots(const uint32_t* d, uint32_t n, uint32_t p, int rw, s
         }
         Item& B = items[c];
         const uint32_t rb = B.r;
-        if (B.pair) {
+        if (B.kind != kSlotOne) {
             B.r += 1;
-            B.pair = false;
+            B.kind = kSlotOne;
         } else {
             ++c;
         }
@@ -686,7 +691,7 @@ void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, int smax, std:
                 uint32_t* eb = slot_area.data() + t0 + 4 * ((size_t)kConeWaves * Q + wq);
                 entry(sw & 1023u, ea);
                 ea[3] = sw;
-                if ((sw >> 20) == kSlotTwo) entry((sw >> 10) & 1023u, eb);
+                if ((sw >> 20) == kSlotTwo || (sw >> 20) == kSlotHalf) entry((sw >> 10) & 1023u, eb);
             }
             l = lo - 1;
         }
@@ -818,13 +823,20 @@ static void validate_blob(const ConeItem& it, uint32_t p, int smax, int rw, cons
                 const uint32_t* eb = w + so + 4 + 4 * ((uint32_t)(kConeWaves * Q) + wq);
                 const uint32_t sw = e[3], ra = sw & 1023u, rb = (sw >> 10) & 1023u, kind = sw >> 20;
                 const int q = (int)g / kConeWaves;
-                const bool two_rows = kind == kSlotTwo || kind == kSlotPair;
-                if (kind > kSlotPair || ra >= n || (two_rows && (rb >= n || 2 * q + 1 >= rw)) ||
-                    (kind == kSlotPair && rb != ra + 1))
+                const bool two_rows = kind != kSlotOne;
+                if (kind > kSlotHalf || ra >= n || (two_rows && (rb >= n || 2 * q + 1 >= rw)) ||
+                    ((kind == kSlotPair || kind == kSlotHalf) && rb != ra + 1))
                     throw std::runtime_error("schedule: bad row slot");
                 if (seen[ra]++ || (two_rows && seen[rb]++)) throw std::runtime_error("schedule: row slot covers a row twice");
                 check_entry(e);
-                if (kind == kSlotTwo) check_entry(eb);
+                if (kind == kSlotTwo || kind == kSlotHalf) check_entry(eb);
+                // a half's rows share the head term: the same head source
+                // offsets (and, two levels, the same head-tail roll), not carried
+                if (kind == kSlotHalf &&
+                    ((two ? (e[0] != eb[0] || (e[2] & 1023u) != (eb[2] & 1023u))
+                          : ((e[0] & 0xFFFFu) != (eb[0] & 0xFFFFu))) ||
+                     (!two && (((e[2] >> 30) & 1u) || ((eb[2] >> 30) & 1u)))))
+                    throw std::runtime_error("schedule: row half without a shared head term");
             }
             for (uint32_t r = 0; r < n; ++r)
                 if (!seen[r]) throw std::runtime_error("schedule: row-slot table misses a row");
@@ -845,10 +857,16 @@ static void validate_blob(const ConeItem& it, uint32_t p, int smax, int rw, cons
         for (uint32_t g = 0; g < ns; ++g) {
             const uint32_t sw = w[so + 1 + g], ra = sw & 1023u, rb = (sw >> 10) & 1023u, kind = sw >> 20;
             const int q = (int)g / kConeWaves;
-            const bool two_rows = kind == kSlotTwo || kind == kSlotPair;
-            if (kind > kSlotPair || ra >= n || (two_rows && (rb >= n || 2 * q + 1 >= rw)))
+            const bool two_rows = kind != kSlotOne;
+            if (kind > kSlotHalf || ra >= n || (two_rows && (rb >= n || 2 * q + 1 >= rw)))
                 throw std::runtime_error("schedule: bad row slot");
             if (seen[ra]++ || (two_rows && seen[rb]++)) throw std::runtime_error("schedule: row slot covers a row twice");
+            if (kind == kSlotHalf) {
+                const uint32_t a = d[ra], b = d[rb];
+                if (rb != ra + 1 || ((a ^ b) & 1023u) || ((a >> 10) & 1023u) == kCarriedRow ||
+                    ((b >> 10) & 1023u) == kCarriedRow)
+                    throw std::runtime_error("schedule: row half without a shared head row");
+            }
             if (kind == kSlotPair) {
                 const uint32_t a = d[ra], b = d[rb];
                 if (rb != ra + 1 || ((a ^ b) & 0xFFFFFu) || ((a >> 10) & 1023u) == kCarriedRow ||
