@@ -260,7 +260,7 @@ void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStrea
             r.moved = L.moved_bytes * batch;
             ck(hipEventRecord(r.a, s), "hipEventRecord");
         }
-        ck(launch_cone(a, L.smax, L.rw, s), "cone_kernel");
+        ck(launch_cone(a, L.smax, L.rw, L.wide_snr != 0, s), "cone_kernel");
         if (prof) {
             ck(hipEventRecord(r.b, s), "hipEventRecord");
             std::lock_guard<std::mutex> lk(g_prof.mu);
@@ -392,7 +392,8 @@ rt_plan* make_plan(size_t size, double tsamp, const uint64_t* widths, size_t nw,
             xf.push_back(X);
         }
         // scratch budget per ping/pong buffer and trial (scratch_budget_floats)
-        build_exec_plan(xf, true, (uint32_t)nw, scratch_budget_floats(), P->dp.ex);
+        const uint32_t wmax = P->widths.empty() ? 0u : *std::max_element(P->widths.begin(), P->widths.end());
+        build_exec_plan(xf, true, (uint32_t)nw, scratch_budget_floats(), P->dp.ex, wmax);
         P->dp.upload();
         ck(hipMalloc(&P->d_flag, sizeof(int)), "hipMalloc");
         ck(hipMemset(P->d_flag, 0, sizeof(int)), "hipMemset");

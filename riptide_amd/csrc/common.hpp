@@ -63,6 +63,38 @@ constexpr int kMaxLevels = 11;              // merge levels of any unit (whole u
 constexpr int kMaxRanges = (1 << (kMaxTileLevels + 1)) - 1;
 constexpr int kMaxWidths = 32;              // boxcar widths handled by the fused S/N epilogue
 constexpr int kSnrChunk = 17;               // S/N epilogue: columns per lane held in registers
+// S/N epilogue (ffa_kernels.hip snr_rows): widths <= kSnrWin from a
+// register window; chunk columns per lane of the register-window path
+constexpr int kSnrWin = 12;
+#ifndef RT_SNR_MAX_CHUNK
+#define RT_SNR_MAX_CHUNK 17
+#endif
+constexpr int kSnrMaxChunk = RT_SNR_MAX_CHUNK;
+// Widths past the register window as plain LDS windows: a final level whose
+// row stride holds the wrapped prefix c[p + e] = c[e] + sum for e < wmax
+// after each row, so every lane's column j0 + t + w (t < its chunk) is a
+// plain read (the planner caps final tiles so their rows fit at this stride:
+// plan.cpp final_tile_cap).  A/B: DESIGN.md section 3.1.
+#ifndef RT_SNR_WIDE_EXT
+#define RT_SNR_WIDE_EXT 1
+#endif
+RT_HD inline int snr_wide_stride(int p, int wmax)
+{
+    return p + (wmax > kSnrMaxChunk ? wmax : kSnrMaxChunk);
+}
+RT_HD inline bool snr_wide_ok(int p, int q, int wmax)
+{
+    return wmax > kSnrWin && wmax < p && q >= snr_wide_stride(p, wmax);
+}
+// S/N lane-group size G of a row of p bins: the smallest power of two >= 8
+// whose chunks ((p + G - 1) / G, made odd) fit kSnrMaxChunk columns.  The
+// wide path runs in the 16-lane groups (p = 137-272).
+RT_HD constexpr int snr_group(int p)
+{
+    int G = 8;
+    while (G < 64 && ((((p + G - 1) / G) | 1) > kSnrMaxChunk)) G <<= 1;
+    return G;
+}
 constexpr int kStageRegs = kConeBuffers == 2 ? 25 : (kConeWgsPerCu == 3 ? 60 : 45);   // merge: staged values per lane (rows x slots)
 constexpr int kMaxSlots = 45;               // merge: 64-bin slots per row (p <= 2880)
 constexpr int kMaxRowsPerWave = 24;         // merge: staged rows per wave

@@ -1280,13 +1280,7 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
 // (the wrap c[p + j] = c[j] + sum applied once per element) and evaluates
 // every width w <= kSnrWin from registers.  Wider rows and wider widths use
 // the general path (shuffles, LDS reads per width).
-constexpr int kSnrWin = 12;
-// S/N chunk columns per lane held in registers (and the window path), by the
-// register budget of the block size
-#ifndef RT_SNR_MAX_CHUNK
-#define RT_SNR_MAX_CHUNK 17
-#endif
-constexpr int kSnrMaxChunk = RT_SNR_MAX_CHUNK;
+// (kSnrWin, kSnrMaxChunk: common.hpp)
 // rows per lane and S/N pass for 16-lane row groups (p = 129-272).  A/B
 // (ms per cfg2 trial): 2 rows (one pass per final unit instead of two,
 // independent chains interleaved) 9.13 vs 8.87 -- the doubled register
@@ -1621,7 +1615,7 @@ __device__ __forceinline__ float grp_allmax(float v)
 // NR rows per lane and pass (NR = 2: the lane's rows r and r + 512/G are
 // independent chains interleaved in one instruction stream, and half as many
 // row passes -- barriers, DPP scans -- per unit).
-template <int CH, int G, int NR = 1>
+template <int CH, int G, int NR = 1, bool WIDE = false>
 __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, float* data, int q, const int* wl,
                                          int nev, int c, int tid, const float* whb, unsigned long long* tl,
                                          bool zpad = false)
@@ -1632,6 +1626,10 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
     // rows with room for the wrapped prefix extension (final-pass output
     // levels at the S/N stride); only the register-window path uses it
     const bool ext = CH <= kSnrMaxChunk && q >= p + kSnrWin;
+    // WIDE (the caller checked snr_wide_ok): every width past the register
+    // window read as a plain LDS window, the wrapped prefix stored up to
+    // p + wmax
+    const int next = WIDE ? wl[kMaxWidths] : kSnrWin;   // wrapped prefix words stored past p
     // rows with room past p for a lane's whole CH-column prefix write
     const bool wfull = q >= p + CH;
     // lanes past the row keep their natural chunk start g * c (their
@@ -1770,19 +1768,24 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
             }
         }
         // rows at a stride q >= p + kSnrWin: the wrapped prefix c[p + j] =
-        // c[j] + sum (kernels.hpp:88-97, j < kSnrWin) stored after the row by
-        // its own lanes (the wave's LDS accesses complete in order), so the
-        // window reads below take c[j0 .. j0 + CH + kSnrWin) without a wrap
+        // c[j] + sum (kernels.hpp:88-97, j < kSnrWin, or j < wmax on the wide
+        // stride) stored after the row by its own lanes (the wave's LDS
+        // accesses complete in order), so the window reads below take
+        // c[j0 .. j0 + CH + kSnrWin) -- and c[j0 + w ..] -- without a wrap
         if (ext) {
 #pragma unroll
             for (int k = 0; k < NR; ++k) {
                 float* const rb = data + min(r[k], nev - 1) * q;
-#pragma unroll
-                for (int e0 = 0; e0 < kSnrWin; e0 += G) {
-                    const int e = e0 + g;
-                    if (active[k] && e < kSnrWin)
+                auto put = [&](int e) {
+                    if (active[k] && e < next)
                         *(volatile __attribute__((address_space(3))) float*)(rb + p + e) =
                             __fadd_rn(lds_ld((lds_cptr)(rb + e)), sum[k]);
+                };
+                if constexpr (WIDE) {
+                    for (int e0 = 0; e0 < next; e0 += G) put(e0 + g);
+                } else {
+#pragma unroll
+                    for (int e0 = 0; e0 < kSnrWin; e0 += G) put(e0 + g);
                 }
             }
         }
@@ -1905,6 +1908,43 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
             const int w = __builtin_amdgcn_readlane(wlane, (int)iw);
             if (CH <= kSnrMaxChunk && w <= kSnrWin) continue;
             float dmax[NR];
+            if constexpr (CH <= kSnrMaxChunk) {
+                // c[j0 + w + t] for the lane's columns t at immediate offsets:
+                // WIDE, inside the row or its stored extension; else the
+                // wrap (j >= p) as a second base za - p and the addend sum
+                // (+0.0 before the wrap point: exact, the prefix values are
+                // never -0.0).  Columns past the chunk read words whose
+                // differences with cp = +inf are dropped.
+#pragma unroll
+                for (int k = 0; k < NR; ++k) {
+                    lds_cptr za = (lds_cptr)(crow[k] + j0 + w);
+                    lds_cptr zb = za - p;
+                    asm("" : "+v"(za), "+v"(zb));
+                    float d[CH];
+                    if constexpr (WIDE) {
+#pragma unroll
+                        for (int t = 0; t < CH; ++t) d[t] = __fsub_rn(lds_ld(za + t), cp[k][t]);   // diff_max, kernels.hpp:50-60
+                    } else {
+                        const int tw = p - j0 - w;        // first wrapped column
+                        float x[CH], ad[CH];
+#pragma unroll
+                        for (int t = 0; t < CH; ++t) {
+                            const bool wrap = t >= tw;
+                            ad[t] = wrap ? sum[k] : 0.0f;
+                            x[t] = lds_ld((wrap ? zb : za) + t);
+                        }
+#pragma unroll
+                        for (int t = 0; t < CH; ++t) d[t] = __fsub_rn(__fadd_rn(x[t], ad[t]), cp[k][t]);
+                    }
+                    float m = d[0];
+#pragma unroll
+                    for (int t = 1; t + 1 < CH; t += 2) m = fmaxf(m, fmaxf(d[t], d[t + 1]));
+                    if constexpr (CH % 2 == 0) m = fmaxf(m, d[CH - 1]);
+                    dmax[k] = m;
+                }
+                emit(iw, dmax);
+                continue;
+            }
             const int last = max(cnt - 1, 0);
 #pragma unroll
             for (int k = 0; k < NR; ++k) {
@@ -1948,12 +1988,6 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
 // Phase-bin range [lo, hi] a cone kernel variant runs, and the S/N lane-group
 // size G of a row of p bins: the epilogue instantiates only the row shapes its
 // variant can meet (smaller kernels; the rest is compiled out).
-constexpr int snr_group(int p)
-{
-    int G = 8;
-    while (G < 64 && ((((p + G - 1) / G) | 1) > kSnrMaxChunk)) G <<= 1;
-    return G;
-}
 constexpr int variant_pmin(int smax) { return smax == kPack2 ? 1 : (smax <= 5 ? 64 * (smax - 1) + 1 : (smax == 8 ? 321 : (smax == 16 ? 513 : 1025))); }
 constexpr int variant_pmax(int smax) { return smax == kPack2 ? 32 : (smax <= 5 ? 64 * smax : (smax == 8 ? 512 : (smax == 16 ? 1024 : 64 * kMaxSlots))); }
 constexpr bool variant_has_group(int smax, int G)
@@ -1961,7 +1995,7 @@ constexpr bool variant_has_group(int smax, int G)
     return snr_group(variant_pmin(smax)) <= G && G <= snr_group(variant_pmax(smax));
 }
 
-template <int SMAX>
+template <int SMAX, bool WIDE = false>
 __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& U, float* data, int q, const int* wl,
                                              int nrows, int tid, float* whb, unsigned long long* tl, bool zpad = false)
 {
@@ -1995,6 +2029,12 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
         }
         if constexpr (variant_has_group(SMAX, 16)) {
             if (G == 16) {
+                if constexpr (WIDE) {
+                    if (snr_wide_ok(p, q, wl[kMaxWidths])) {
+                        snr_rows<kSnrMaxChunk, 16, RT_SNR_ROWS, true>(a, U, data, q, wl, nev, c, tid, whb, tl, zpad);
+                        return;
+                    }
+                }
                 snr_rows<kSnrMaxChunk, 16, RT_SNR_ROWS>(a, U, data, q, wl, nev, c, tid, whb, tl, zpad);
                 return;
             }
@@ -2086,13 +2126,18 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
 #ifndef RT_SNR_ZPAD
 #define RT_SNR_ZPAD 0
 #endif
-template <int SMAX, int RWT = 0>
+// WIDE: final units whose S/N takes the widths past its register window as
+// plain LDS windows (snr_wide_ok; a separate instantiation, so the plans
+// without such widths run code without it)
+template <int SMAX, int RWT = 0, bool WIDE = false>
 __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(ConeArgs a)
 {
     constexpr int RW = RWT ? RWT : merge_rows_per_wave(SMAX);   // register rows per wave
     __shared__ __attribute__((aligned(16))) float data[kConeBuffers][kLdsBufFloats + kLdsPadFloats];
     __shared__ __attribute__((aligned(16))) uint32_t aux[kConeBuffers][kAuxWords];   // tile units: the host blob
-    __shared__ int wl[kMaxWidths];   // boxcar widths: LDS reads never wait on the S/N stores in flight
+    // boxcar widths (LDS reads never wait on the S/N stores in flight), then
+    // the widest of them
+    __shared__ int wl[kMaxWidths + 1];
     __shared__ float whb[2 * kMaxWidths];   // S/N: h + b and b per width
 
     const int tid = threadIdx.x;
@@ -2110,6 +2155,11 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
     uint32_t u = blockIdx.x;
     if (u >= total) return;
     if (tid < (int)a.num_widths) wl[tid] = (int)a.widths[tid];   // visible after the first barrier
+    if (tid == 0) {
+        uint32_t wm = 0;
+        for (uint32_t i = 0; i < a.num_widths; ++i) wm = max(wm, a.widths[i]);
+        wl[kMaxWidths] = (int)wm;
+    }
     const bool dma = !(a.flags & kConeDiagNoLand);
     int b = 0;
     bool ok;
@@ -2168,8 +2218,19 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
                 // extension), else >= p + kSnrWin (the extension only)
                 const int qa = p + kSnrMaxChunk + ((16 - ((p + kSnrMaxChunk) & 31)) & 31);
                 const int qb = p + kSnrWin + ((16 - ((p + kSnrWin) & 31)) & 31);
-                if (!st && L > 0 && C.slots && (a.flags & kConeFuse2) && (a.flags & kConeSnrStride))
+                if (!st && L > 0 && C.slots && (a.flags & kConeFuse2) && (a.flags & kConeSnrStride)) {
                     qout = n0 * qa <= kLdsDataFloats ? qa : (n0 * qb <= kLdsDataFloats ? qb : p);
+                    // widths past the register window: a stride with room for
+                    // their plain-LDS windows (snr_wide_stride), = 16 (mod 32)
+                    // where that fits too
+                    const int wmax = wl[kMaxWidths];
+                    if (WIDE && snr_group(p) == 16 && wmax > kSnrWin && wmax < p) {
+                        const int qw = snr_wide_stride(p, wmax);
+                        const int qwp = qw + ((16 - (qw & 31)) & 31);
+                        if (n0 * qwp <= kLdsDataFloats) qout = qwp;
+                        else if (n0 * qw <= kLdsDataFloats) qout = qw;
+                    }
+                }
             }
             // the S/N's chunks read without column masks (zero-padded rows):
             // a final pass whose output level the row-slot write-back stores
@@ -2192,9 +2253,9 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
                 }
             } else {
 #ifdef RT_STAMPS
-                if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX>(a, U, obase, qout, wl, n0, tid, whb, tl, zpad);
+                if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(a, U, obase, qout, wl, n0, tid, whb, tl, zpad);
 #else
-                if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX>(a, U, obase, qout, wl, n0, tid, whb, nullptr, zpad);
+                if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(a, U, obase, qout, wl, n0, tid, whb, nullptr, zpad);
 #endif
             }
         }
@@ -2237,7 +2298,7 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
 
 // Persistent grid: kConeWgsPerCu workgroups per CU (RIPTIDE_AMD_CONE_PERSIST=0:
 // one workgroup per unit, for A/B).
-hipError_t launch_cone(const ConeArgs& args, uint32_t smax, uint32_t rw, hipStream_t s)
+hipError_t launch_cone(const ConeArgs& args, uint32_t smax, uint32_t rw, bool wide_snr, hipStream_t s)
 {
     if (!args.num_items || !args.batch) return hipSuccess;
     const uint64_t total = (uint64_t)args.num_items * args.batch;
@@ -2265,14 +2326,20 @@ hipError_t launch_cone(const ConeArgs& args, uint32_t smax, uint32_t rw, hipStre
         }
         break;
     case 2: hipLaunchKernelGGL(cone_kernel<2>, g, b, 0, s, args); break;
-    case 3: hipLaunchKernelGGL(cone_kernel<3>, g, b, 0, s, args); break;
+    case 3:
+        if (wide_snr) hipLaunchKernelGGL((cone_kernel<3, 0, true>), g, b, 0, s, args);
+        else hipLaunchKernelGGL(cone_kernel<3>, g, b, 0, s, args);
+        break;
     case 4:
         switch (rw) {
         case 5: hipLaunchKernelGGL((cone_kernel<4, 5>), g, b, 0, s, args); break;
         case 6: hipLaunchKernelGGL((cone_kernel<4, 6>), g, b, 0, s, args); break;
         case 7: hipLaunchKernelGGL((cone_kernel<4, 7>), g, b, 0, s, args); break;
         case 8: hipLaunchKernelGGL((cone_kernel<4, 8>), g, b, 0, s, args); break;
-        default: hipLaunchKernelGGL(cone_kernel<4>, g, b, 0, s, args); break;
+        default:
+            if (wide_snr) hipLaunchKernelGGL((cone_kernel<4, 0, true>), g, b, 0, s, args);
+            else hipLaunchKernelGGL(cone_kernel<4>, g, b, 0, s, args);
+            break;
         }
         break;
     case 5:
@@ -2281,7 +2348,10 @@ hipError_t launch_cone(const ConeArgs& args, uint32_t smax, uint32_t rw, hipStre
         case 6: hipLaunchKernelGGL((cone_kernel<5, 6>), g, b, 0, s, args); break;
         case 7: hipLaunchKernelGGL((cone_kernel<5, 7>), g, b, 0, s, args); break;
         case 8: hipLaunchKernelGGL((cone_kernel<5, 8>), g, b, 0, s, args); break;
-        default: hipLaunchKernelGGL(cone_kernel<5>, g, b, 0, s, args); break;
+        default:
+            if (wide_snr) hipLaunchKernelGGL((cone_kernel<5, 0, true>), g, b, 0, s, args);
+            else hipLaunchKernelGGL(cone_kernel<5>, g, b, 0, s, args);
+            break;
         }
         break;
     case 8: hipLaunchKernelGGL(cone_kernel<8>, g, b, 0, s, args); break;

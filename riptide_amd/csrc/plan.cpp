@@ -187,7 +187,9 @@ static double pass_weight()
     return 100.0;
 }
 
-static void plan_transform(const FfaXform& X, uint32_t xi, int smax, std::vector<PassItems>& passes)
+// final_kmax: output rows per final-pass tile at most (the wide S/N stride,
+// snr_wide_stride); 0 = no cap.
+static void plan_transform(const FfaXform& X, uint32_t xi, int smax, uint32_t final_kmax, std::vector<PassItems>& passes)
 {
     passes.clear();
     const uint32_t m = X.m, p = X.p;
@@ -236,17 +238,18 @@ static void plan_transform(const FfaXform& X, uint32_t xi, int smax, std::vector
         nodes_at_depth(m, dtop, nodes);
         PassItems pass;
         const int guess = std::max(1, C - (2 << L) - 2);
+        const uint32_t kmax = k == npass - 1 && final_kmax ? final_kmax : ~0u;
         for (const Node& n : nodes) {
             uint32_t s0 = 0;
             while (s0 < n.size) {
-                uint32_t K = std::min<uint32_t>((uint32_t)guess, n.size - s0);
+                uint32_t K = std::min<uint32_t>(std::min<uint32_t>((uint32_t)guess, kmax), n.size - s0);
                 ConeNeed need = cone_need(n.size, s0, s0 + K, L, p);
                 while (K > 1 && !fits(need, p, smax)) {
                     K -= std::max<uint32_t>(1, K / 32);
                     need = cone_need(n.size, s0, s0 + K, L, p);
                 }
                 if (!fits(need, p, smax)) throw std::invalid_argument("cone tile does not fit in LDS");
-                while (s0 + K < n.size) {
+                while (s0 + K < n.size && K < kmax) {
                     ConeNeed nn = cone_need(n.size, s0, s0 + K + 1, L, p);
                     if (!fits(nn, p, smax)) break;
                     need = nn;
@@ -281,8 +284,29 @@ static double item_cost(const ConeItem& it, const FfaXform& X)
     return rows * (double)X.p * ((double)it.levels + 2.0);
 }
 
+// Output rows per final tile that leave room for the wide S/N stride (widths
+// past the S/N register window read as plain LDS windows, common.hpp
+// snr_wide_stride), or 0 (no cap: no such widths, or the variant has no wide
+// path).  RIPTIDE_AMD_SNR_WIDE=0 drops the cap (A/B).
+static bool wide_snr(const FfaXform& X, int smax, bool snr_epilogue, uint32_t max_width)
+{
+    if (!RT_SNR_WIDE_EXT || !snr_epilogue || smax > 5 || smax == kPack2) return false;
+    if (snr_group((int)X.p) != 16 || (int)max_width <= kSnrWin || max_width >= X.p) return false;
+    if (const char* e = std::getenv("RIPTIDE_AMD_SNR_WIDE"))
+        if (e[0] == '0') return false;
+    return true;
+}
+
+static uint32_t final_tile_cap(const FfaXform& X, int smax, bool snr_epilogue, uint32_t max_width)
+{
+    if (!wide_snr(X, smax, snr_epilogue, max_width)) return 0;
+    const int q = snr_wide_stride((int)X.p, (int)max_width);
+    const int k = kLdsDataFloats / q;
+    return k >= 8 ? (uint32_t)k : 0;
+}
+
 void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uint32_t num_widths,
-                     uint64_t scratch_budget, ExecPlan& out)
+                     uint64_t scratch_budget, ExecPlan& out, uint32_t max_width)
 {
     out = ExecPlan();
     out.xf = xforms;
@@ -311,7 +335,8 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
         sched.assign(g1 - g0, {});
         uint32_t gpasses = 0;
         for (size_t i = g0; i < g1; ++i) {
-            plan_transform(out.xf[i], (uint32_t)i, merge_slots(out.xf[i].p), sched[i - g0]);
+            plan_transform(out.xf[i], (uint32_t)i, merge_slots(out.xf[i].p),
+                           final_tile_cap(out.xf[i], merge_slots(out.xf[i].p), snr_epilogue, max_width), sched[i - g0]);
             gpasses = std::max<uint32_t>(gpasses, (uint32_t)sched[i - g0].size());
         }
         out.max_passes = std::max(out.max_passes, gpasses);
@@ -343,6 +368,7 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
                         out.items.push_back(it);
                     }
                     const double cells = (double)X.m * X.p;
+                    if (last && wide_snr(X, bucket, snr_epilogue, max_width)) L.wide_snr = 1;
                     L.cells += (uint64_t)X.m * X.p;
                     L.alg_bytes += 4.0 * cells + ((last && snr_epilogue) ? 4.0 * X.rows_eval * num_widths : 4.0 * cells);
                     L.moved_bytes += sp[k].read + ((last && snr_epilogue) ? 4.0 * X.rows_eval * num_widths : sp[k].written);

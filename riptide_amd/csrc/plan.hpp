@@ -53,6 +53,7 @@ struct Launch {
     uint32_t group = 0, pass = 0;
     uint32_t smax = 0;               // cone kernel variant: merge_slots() of every transform in the launch
     uint32_t rw = 0;                 // register rows per wave of the variant (0: merge_rows_per_wave(smax))
+    uint32_t wide_snr = 0;           // final units whose S/N reads wide widths as plain LDS windows (WIDE variant)
     double alg_bytes = 0;            // 4mp read + (4mp | 4*rows_eval*W) write
     double moved_bytes = 0;          // bytes the items actually read + write (cone overlap incl.)
     uint64_t cells = 0;              // sum m*p of the transforms in this launch
@@ -96,9 +97,10 @@ void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, int smax, std:
 // filled in by the caller).  With snr_epilogue the last pass of every
 // transform writes S/N rows; otherwise it writes the transform into `ping`.
 // Transforms are grouped so that each group's scratch fits scratch_budget
-// floats per buffer; a group's passes are consecutive launches.
+// floats per buffer; a group's passes are consecutive launches.  max_width
+// (the widest boxcar, 0 = unknown) caps final tiles for the S/N's wide stride.
 void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uint32_t num_widths,
-                     uint64_t scratch_budget, ExecPlan& out);
+                     uint64_t scratch_budget, ExecPlan& out, uint32_t max_width = 0);
 
 // Schedule invariants (every item fits its LDS / register budget and stays
 // inside its node, the final pass of every transform covers rows [0, m) once,

@@ -259,6 +259,33 @@ def test_batch_matches_single(rt):
         assert np.array_equal(dn[b].cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("ducy_max, widths", [(0.2, None), (0.35, [1, 2, 5, 13, 40, 77, 91])])
+def test_wide_snr_matches_window_path(monkeypatch, ducy_max, widths):
+    """Final units whose S/N reads the widths past its 12-column register
+    window as plain LDS windows (the WIDE kernel instances, final tiles capped
+    to the wide row stride) give exactly the S/N of the wrapped-window path
+    (RIPTIDE_AMD_SNR_WIDE=0), which the golden tests pin to the oracle; on a
+    cfg3-shaped multi-pass schedule, incl. widths up to 91 of 240 bins and
+    unsorted widths."""
+    import torch
+    from riptide_amd import engine, libcpp
+    n, tsamp = 1 << 19, 256e-6
+    x = np.stack([inputs.with_signal(n, tsamp, s, 0.71, 9.0) for s in range(3)])
+    d = torch.from_numpy(x).cuda()
+    out = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("RIPTIDE_AMD_SNR_WIDE", v)
+        if widths is None:
+            plan = engine.PeriodogramPlan.for_search(n, tsamp, 0.2, 5.0, 240, 260, ducy_max=ducy_max)
+        else:
+            plan = engine.PeriodogramPlan(n, tsamp, list(reversed(widths)), 0.2, 5.0, 240, 260)
+        out[v] = plan.run(d).cpu().numpy()
+    assert np.array_equal(out["1"], out["0"])
+    w = [int(v) for v in plan.widths]
+    _, _, single = libcpp.periodogram(x[1], tsamp, np.asarray(w, dtype=np.uint64), 0.2, 5.0, 240, 260)
+    assert np.array_equal(out["1"][1], single)
+
+
 def test_fused_ladder_matches_per_rung(monkeypatch):
     """The fused downsampling ladder (one read of the series for every rung)
     produces exactly the per-rung kernel's leaves, hence identical S/N."""

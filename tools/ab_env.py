@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""A/B of one run-time environment knob of the engine (read per launch, e.g.
-RIPTIDE_AMD_TRIALS_PER_WG) on one BASELINE config: ms per trial of the
+"""A/B of one environment knob of the engine (read per launch, or by the
+planner: one plan per value) on one BASELINE config: ms per trial of the
 periodogram for each value, two rounds, and whether the S/N equals the first
 value's.
 
@@ -25,15 +25,22 @@ def main():
     c = {k["name"]: k for k in CONFIGS}[sys.argv[3] if len(sys.argv) > 3 else "cfg2"]
     B = int(sys.argv[4]) if len(sys.argv) > 4 else 16
     n = c["n"]
-    plan = engine.PeriodogramPlan.for_search(n, c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"],
-                                             ducy_max=c["ducy_max"])
+    # one plan per value, built with the knob set (planner knobs are read
+    # when a plan is built, kernel knobs per launch)
+    plans = {}
+    for v in vals:
+        os.environ[var] = v
+        plans[v] = engine.PeriodogramPlan.for_search(n, c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"],
+                                                     ducy_max=c["ducy_max"])
+    plan = plans[vals[0]]
     x = torch.randn((B, n), device="cuda", dtype=torch.float32)
     out = torch.empty((B, plan.length, plan.num_widths), device="cuda", dtype=torch.float32)
-    ws = torch.empty(plan.workspace_bytes(B), dtype=torch.uint8, device="cuda")
+    ws = torch.empty(max(p.workspace_bytes(B) for p in plans.values()), dtype=torch.uint8, device="cuda")
     ref = None
     for rnd in range(2):
         for v in vals:
             os.environ[var] = v
+            plan = plans[v]
             plan.run(x, out=out, workspace=ws)
             torch.cuda.synchronize()
             engine.profile_reset()
