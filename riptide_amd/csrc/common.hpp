@@ -165,6 +165,12 @@ RT_HD inline int merge_slots(uint32_t p)
 }
 
 // 64-lane slots per register row of a merge variant, and rows per slot
+// Row stride of the merge levels above the fill in the short-row variant
+// (kPack2, ffa_kernels.hip merge_step_tasks): odd for p >= 8.
+#ifndef RT_PACK_TASKS
+#define RT_PACK_TASKS 1
+#endif
+RT_HD inline int pack_stride(int p) { return RT_PACK_TASKS && p >= 8 ? (p | 1) : p; }
 RT_HD constexpr int slot_count(int smax) { return smax == kPack2 ? 1 : smax; }
 RT_HD constexpr int row_pack(int smax) { return smax == kPack2 ? 2 : 1; }
 

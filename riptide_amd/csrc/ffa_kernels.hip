@@ -369,7 +369,8 @@ __device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t u, uin
             // at the end of the level buffer, above the fill and every level
             // (validate_exec_plan; pack_blob_words)
             C.aux = reinterpret_cast<uint32_t*>(buf + kLdsBufFloats) - words;
-            ok = ok && C.nb <= cap && 4 * U.fill_chunks + words <= kLdsBufFloats && C.nb * p + words <= kLdsBufFloats;
+            ok = ok && C.nb <= cap && 4 * U.fill_chunks + words <= kLdsBufFloats &&
+                 C.nb * pack_stride(p) + words <= kLdsBufFloats;
         } else {
             ok = ok && C.nb <= cap && C.entries <= kDescEntries && words <= kAuxWords;
         }
@@ -1154,6 +1155,123 @@ __device__ __forceinline__ void store_rows_lanes(const float (&v)[RW][1], int p,
     }
 }
 
+// kPack2 rows of p >= 8 bins as (row, 8-bin segment) tasks, one per lane
+// (RT_PACK_TASKS): task t = tid + kConeBlock * i is row t / segs, segment
+// t % segs, bins j0 .. j0 + 7 with j0 = min(8 * seg, p - 8) (the last
+// segment of a row overlaps the one before it when 8 does not divide p:
+// those bins are computed twice, identically, and written twice with the
+// same value).  A lane resolves its row's entry once for its 8 bins, the
+// head read is the row plus an immediate offset, and a rolled read picks one
+// of two bases (before / after the wrap point) per bin: a third of the VALU
+// of the lane-per-bin layout, where every lane decoded its row's entry and
+// wrapped its own index.  Tasks past the level's rows redo the last task
+// (same values, same addresses).  Levels above the fill at the odd stride
+// qs = p | 1 (the 32-lane halves of a read or write then hit distinct banks
+// for distinct rows).
+#ifndef RT_PACK_TASKS
+#define RT_PACK_TASKS 1
+#endif
+constexpr int kPackSeg = 8;
+constexpr int kPackTasks = 3;                 // tasks per lane: kMaxRows rows x 4 segments
+static_assert(kMaxRows * 4 <= kPackTasks * kConeBlock, "short-row tasks per lane");
+RT_HD inline int pack_segments(int p) { return (p + kPackSeg - 1) / kPackSeg; }
+
+// task -> (row, first bin); segs in 1..4, t < 2^11
+__device__ __forceinline__ void pack_task(int t, int segs, int p, int& r, int& j0)
+{
+    const uint32_t m = segs == 1 ? (1u << 20) : (segs == 2 ? (1u << 19) : (segs == 3 ? 349526u : (1u << 18)));
+    r = (int)(__umul24((uint32_t)t, m) >> 20);
+    j0 = min((t - r * segs) * kPackSeg, p - kPackSeg);
+}
+
+// x[e] = row[(j0 + s + e) mod p] of the row at LDS offset o (j0 + e < p, s < p)
+__device__ __forceinline__ void pack_rolled(lds_cptr sp, int o, int j0, int s, int p, float (&x)[kPackSeg])
+{
+    lds_cptr lo = sp + o + j0 + s;
+    lds_cptr hi = lo - p;
+    const int w = p - j0 - s;                 // first wrapped element
+#pragma unroll
+    for (int e = 0; e < kPackSeg; ++e) x[e] = lds_ld((e >= w ? hi : lo) + e);
+}
+
+template <bool TWO, bool FIRST>
+__device__ __forceinline__ void merge_step_tasks(const UnitCtx& C, const float* src, int p, int qs, int lo, int tid,
+                                                 int nrows, float (&v)[kPackTasks][kPackSeg], const int* loff)
+{
+    const int segs = pack_segments(p);
+    const int ntask = nrows * segs;
+    const uint32_t* const desc = desc_table(C);
+    const int dl = TWO ? 0 : desc_offset(C, lo);
+    const uint2* const step = reinterpret_cast<const uint2*>(TWO ? slot_table(C, lo) : C.aux);
+    const lds_cptr sp = (lds_cptr)src;
+#pragma unroll
+    for (int i = 0; i < kPackTasks; ++i) {
+        if (kConeBlock * i < ntask) {
+            int r, j0;
+            pack_task(min(tid + kConeBlock * i, ntask - 1), segs, p, r, j0);
+            float x0[kPackSeg], x1[kPackSeg];
+            if constexpr (TWO) {
+                // the host-resolved row: source rows q0..q3 of level lo + 2, rolls
+                const uint2 e = step[r];
+                const uint32_t q0 = e.x & 1023u, q1 = (e.x >> 10) & 1023u, q2 = (e.x >> 20) & 1023u, q3 = e.y & 1023u;
+                const int sH = (int)((e.y >> 10) & 63u), sh = (int)((e.y >> 16) & 63u), sTT = (int)((e.y >> 22) & 63u);
+                const int o0 = FIRST ? loff[q0] : (int)__umul24(q0, (uint32_t)qs);
+                const int o1 = FIRST ? loff[q1] : (int)__umul24(q1, (uint32_t)qs);
+                const int o2 = FIRST ? loff[q2] : (int)__umul24(q2, (uint32_t)qs);
+                const int o3 = FIRST ? loff[q3] : (int)__umul24(q3, (uint32_t)qs);
+                float x2[kPackSeg], x3[kPackSeg];
+                const lds_cptr h0 = sp + o0 + j0;
+#pragma unroll
+                for (int k = 0; k < kPackSeg; ++k) x0[k] = lds_ld(h0 + k);
+                pack_rolled(sp, o1, j0, sH, p, x1);
+                pack_rolled(sp, o2, j0, sh, p, x2);
+                pack_rolled(sp, o3, j0, sTT, p, x3);
+#pragma unroll
+                for (int k = 0; k < kPackSeg; ++k) v[i][k] = __fadd_rn(__fadd_rn(x0[k], x1[k]), __fadd_rn(x2[k], x3[k]));
+            } else {
+                const uint32_t d = desc[dl + r];
+                const uint32_t tc = (d >> 10) & 1023u;
+                const bool car = tc == kCarried;
+                const int sh = (int)(d >> 20);
+                const int ho = FIRST ? loff[d & 1023u] : (int)__umul24(d & 1023u, (uint32_t)qs);
+                const int to = car ? ho : (FIRST ? loff[tc & 1023u] : (int)__umul24(tc, (uint32_t)qs));
+                const lds_cptr h0 = sp + ho + j0;
+#pragma unroll
+                for (int k = 0; k < kPackSeg; ++k) x0[k] = lds_ld(h0 + k);
+                pack_rolled(sp, to, j0, car ? 0 : sh, p, x1);
+                // a carried size-1 node adds -0.0 (x + (-0.0) == x: the reference's copy)
+#pragma unroll
+                for (int k = 0; k < kPackSeg; ++k) v[i][k] = __fadd_rn(x0[k], car ? -0.0f : x1[k]);
+            }
+        }
+    }
+}
+
+template <bool GLOBAL>
+__device__ __forceinline__ void put_tasks(float* base, int q, const float (&v)[kPackTasks][kPackSeg], int p, int tid,
+                                          int nrows, __amdgpu_buffer_rsrc_t rs, uint32_t st_o0)
+{
+    const int segs = pack_segments(p);
+    const int ntask = nrows * segs;
+#pragma unroll
+    for (int i = 0; i < kPackTasks; ++i) {
+        if (kConeBlock * i < ntask) {
+            int r, j0;
+            pack_task(min(tid + kConeBlock * i, ntask - 1), segs, p, r, j0);
+            if constexpr (GLOBAL) {
+                const uint32_t ob = st_o0 + (uint32_t)(r * p + j0) * 4u;
+#pragma unroll
+                for (int k = 0; k < kPackSeg; ++k)
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs, (int)(ob + 4u * k), 0, 0);
+            } else {
+                float* const o = base + r * q + j0;
+#pragma unroll
+                for (int k = 0; k < kPackSeg; ++k) o[k] = v[i][k];
+            }
+        }
+    }
+}
+
 // All merge levels of one unit, deepest first, in place in the dense rows
 // at `base`.  SMAX >= ceil(p/64) slots per row, RW rows per wave
 // (lds_row_capacity(p, SMAX) guarantees ceil(rows/8) <= RW at every level).
@@ -1179,6 +1297,33 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
     // and for a last odd level
     const bool fuse = (flags & kConeFuse2) != 0;
     if constexpr (SMAX == kPack2) {
+        if (RT_PACK_TASKS && p >= kPackSeg) {
+            const int qs = pack_stride(p);
+            for (int l = L - 1; l >= 0;) {
+                const bool two = fuse && l >= 1 && (tile || (node_size >> l) >= 2);
+                const int lo = two ? l - 1 : l;
+                const int nrows = rows_at(C, lo);
+                float v[kPackTasks][kPackSeg];
+                const bool first = l == L - 1;
+                const float* src = first ? src0 : base;
+                if (first) {
+                    if (two) merge_step_tasks<true, true>(C, src, p, qs, lo, tid, nrows, v, loff);
+                    else merge_step_tasks<false, true>(C, src, p, qs, lo, tid, nrows, v, loff);
+                } else {
+                    if (two) merge_step_tasks<true, false>(C, src, p, qs, lo, tid, nrows, v, nullptr);
+                    else merge_step_tasks<false, false>(C, src, p, qs, lo, tid, nrows, v, nullptr);
+                }
+                l = lo - 1;
+                if (lo == 0 && st) {
+                    put_tasks<true>(base, qs, v, p, tid, nrows, rs, st_o0);
+                    return;
+                }
+                if (!(flags & kConeDiagNoBarrier)) lds_barrier();
+                if (!(flags & kConeDiagNoWrite)) put_tasks<false>(base, qs, v, p, tid, nrows, rs, st_o0);
+                if (!(flags & kConeDiagNoBarrier)) lds_barrier();
+            }
+            return;
+        }
         for (int l = L - 1; l >= 0;) {
             const bool two = fuse && l >= 1 && (tile || (node_size >> l) >= 2);
             const int lo = two ? l - 1 : l;
@@ -2212,6 +2357,10 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
             // group, odd chunk strides) then read and write on distinct banks
             // (at stride p they collided on up to 10 of 32 banks)
             int qout = p;
+            // short rows in (row, segment) tasks: every level above the fill
+            // at the odd stride pack_stride(p)
+            if constexpr (SMAX == kPack2)
+                if (L > 0) qout = pack_stride(p);
             if constexpr (SMAX <= 5 && SMAX != kPack2) {
                 // = 16 (mod 32) and >= p + kSnrMaxChunk (room for the S/N's
                 // whole-chunk prefix writes and its wrapped prefix
@@ -2246,9 +2395,10 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
             float* const obase = L > 0 ? buf : buf + (C.table ? uni(bottom_offsets(C)[0]) : C.al);
             if (st) {
                 if (L == 0 || !st_regs) {
+                    const int qst = L > 0 ? qout : p;    // the merged level's LDS row stride
                     for (int r = 0; r < n0; ++r)
                         for (int j = tid; j < p; j += kConeBlock)
-                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(obase[r * p + j]), rs,
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(obase[r * qst + j]), rs,
                                                                   (int)(o0 + (uint32_t)(r * p + j) * 4u), 0, 0);
                 }
             } else {

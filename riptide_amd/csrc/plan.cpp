@@ -167,7 +167,8 @@ static bool fits(const ConeNeed& n, uint32_t p, int smax)
     if (n.degenerate || n.max_rows > lds_row_capacity(p, smax) || n.ranges > kMaxRanges) return false;
     const int fill = 4 * fill_chunks_bound(n.rows_bottom, (int)p, n.runs_bottom);
     if (smax == kPack2)   // the blob at the end of the level buffer (pack_blob_words)
-        return std::max(fill, n.max_floats) + pack_blob_words(n.entries, n.rows_bottom) <= kLdsBufFloats;
+        return std::max(fill, n.max_rows * pack_stride((int)p)) + pack_blob_words(n.entries, n.rows_bottom) <=
+               kLdsBufFloats;
     return n.max_floats <= kLdsDataFloats && fill <= kLdsBufFloats && n.entries <= kDescEntries;
 }
 
@@ -946,7 +947,7 @@ void validate_exec_plan(const ExecPlan& ex, bool snr_epilogue)
                 // blob at the end of the level buffer, clear of the fill and every level
                 if (it.pad == kNoBlob) throw std::runtime_error("schedule: short-row unit without a descriptor table");
                 const uint32_t* h = ex.blob.data() + it.pad;
-                const int top = std::max<int>(4 * (int)h[kHdrFill], rows * (int)X.p);
+                const int top = std::max<int>(4 * (int)h[kHdrFill], rows * pack_stride((int)X.p));
                 if (top + (int)h[kHdrRunOff] > kLdsBufFloats)
                     throw std::runtime_error("schedule: short-row unit and its descriptor table exceed the level buffer");
             } else if (it.mode == kModeTile && (need.entries > kDescEntries || it.pad == kNoBlob)) {
