@@ -1189,6 +1189,9 @@ __device__ __forceinline__ void pack_rolled(lds_cptr sp, int o, int j0, int s, i
 {
     lds_cptr lo = sp + o + j0 + s;
     lds_cptr hi = lo - p;
+    // opaque: one select of the two addresses per element (the element
+    // offset immediate), not a select of 0 / p folded into a shifted add
+    asm("" : "+v"(lo), "+v"(hi));
     const int w = p - j0 - s;                 // first wrapped element
 #pragma unroll
     for (int e = 0; e < kPackSeg; ++e) x[e] = lds_ld((e >= w ? hi : lo) + e);
@@ -1204,9 +1207,12 @@ __device__ __forceinline__ void merge_step_tasks(const UnitCtx& C, const float* 
     const int dl = TWO ? 0 : desc_offset(C, lo);
     const uint2* const step = reinterpret_cast<const uint2*>(TWO ? slot_table(C, lo) : C.aux);
     const lds_cptr sp = (lds_cptr)src;
+    // waves whose tasks all lie past the level skip the block (per wave:
+    // a partly filled block would otherwise run every wave)
+    const int wave0 = tid & ~63;
 #pragma unroll
     for (int i = 0; i < kPackTasks; ++i) {
-        if (kConeBlock * i < ntask) {
+        if (kConeBlock * i + wave0 < ntask) {
             int r, j0;
             pack_task(min(tid + kConeBlock * i, ntask - 1), segs, p, r, j0);
             float x0[kPackSeg], x1[kPackSeg];
@@ -1253,9 +1259,10 @@ __device__ __forceinline__ void put_tasks(float* base, int q, const float (&v)[k
 {
     const int segs = pack_segments(p);
     const int ntask = nrows * segs;
+    const int wave0 = tid & ~63;
 #pragma unroll
     for (int i = 0; i < kPackTasks; ++i) {
-        if (kConeBlock * i < ntask) {
+        if (kConeBlock * i + wave0 < ntask) {
             int r, j0;
             pack_task(min(tid + kConeBlock * i, ntask - 1), segs, p, r, j0);
             if constexpr (GLOBAL) {
