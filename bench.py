@@ -378,6 +378,9 @@ def main():
     ap.add_argument("--files", type=int, default=256, help="cfg5: SIGPROC files per GPU")
     ap.add_argument("--trials", type=int, default=0, help="cfg3: trials in the job (default 1024)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--overlap", type=int, default=0, choices=(0, 1),
+                    help="cfg2: 1 = step k+1's deredden + normalise + downsampling ladder on a second stream "
+                         "while step k's FFA passes run (two workspaces); 0 = one stream")
     args = ap.parse_args()
     if not args.batch:
         args.batch = 32 if args.workload == "cfg3" else 16
@@ -414,14 +417,31 @@ def main():
     dws = torch.empty(engine.deredden_workspace_bytes(c["n"], ws_samples, c["rmed_minpts"], B),
                       dtype=torch.uint8, device=dev)
     snr = torch.empty((B, plan.length, plan.num_widths), dtype=torch.float32, device=dev)
-    pws = torch.empty(plan.workspace_bytes(B), dtype=torch.uint8, device=dev)
+    pws = [torch.empty(plan.workspace_bytes(B), dtype=torch.uint8, device=dev) for _ in range(1 + args.overlap)]
+    s_main = torch.cuda.current_stream(dev)
+    s_prep = torch.cuda.Stream(dev) if args.overlap else s_main
+    ev_prep = [torch.cuda.Event() for _ in pws]
+    ev_done = [torch.cuda.Event() for _ in pws]
 
-    def step():
-        engine.deredden_normalise(raw, ws_samples, c["rmed_minpts"], out=xbuf, workspace=dws)
-        plan.run(xbuf, out=snr, workspace=pws)
+    def run_steps(k_steps):
+        # one step = deredden + normalise + ladder (prep) and the FFA passes +
+        # S/N of one batch; with --overlap the prep of step k + 1 runs on
+        # s_prep while step k's passes run on s_main (workspace k % 2; the
+        # prep of step k + 2 waits for step k's passes to release it)
+        for k in range(k_steps):
+            w = k % len(pws)
+            with torch.cuda.stream(s_prep):
+                if args.overlap and k >= len(pws):
+                    s_prep.wait_event(ev_done[w])
+                engine.deredden_normalise(raw, ws_samples, c["rmed_minpts"], out=xbuf, workspace=dws, stream=s_prep)
+                plan.ladder(xbuf, pws[w], stream=s_prep)
+                ev_prep[w].record(s_prep)
+            s_main.wait_event(ev_prep[w])
+            plan.passes(snr, pws[w], stream=s_main)
+            ev_done[w].record(s_main)
+        s_main.wait_stream(s_prep)
 
-    for _ in range(args.warmup):
-        step()
+    run_steps(args.warmup)
     torch.cuda.synchronize()
     plan.check()                  # device error flag of the warmup runs
     if world > 1:
@@ -430,8 +450,7 @@ def main():
     engine.profile_reset()
     engine.profile_enable(True)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    run_steps(args.steps)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     engine.profile_enable(False)
@@ -473,6 +492,8 @@ def main():
                 "ffa_transforms": stats["transforms"],
                 "cone_launches_per_step": stats["launches"],
                 "scratch_mfloats_per_buffer_trial": float(os.environ["RIPTIDE_AMD_SCRATCH_MFLOATS"]),
+                "streams": "prep (deredden+normalise+ladder of step k+1) || FFA passes of step k" if args.overlap
+                           else "one",
                 "parallelism": f"dm-trials x{world} (independent, weak scaling)",
             },
             "roofline": rf,

@@ -143,6 +143,15 @@ int rt_plan_workspace_bytes(const rt_plan* plan, size_t batch, size_t* bytes);
 int rt_periodogram_device(const rt_plan* plan, const float* d_data, size_t batch, size_t data_stride,
                           float* d_snrs, size_t snr_stride, void* d_workspace, size_t workspace_bytes,
                           void* stream);
+/* rt_periodogram_device in two stream-ordered halves, so a pipelined caller
+ * can run batch k + 1's downsampling ladder (periodogram.hpp:162-168) on one
+ * stream while batch k's FFA passes + S/N run on another: the ladder fills
+ * the workspace's leaf buffer, the passes read it (same workspace, same
+ * batch).  ladder then passes == rt_periodogram_device. */
+int rt_periodogram_ladder_device(const rt_plan* plan, const float* d_data, size_t batch, size_t data_stride,
+                                 void* d_workspace, size_t workspace_bytes, void* stream);
+int rt_periodogram_passes_device(const rt_plan* plan, size_t batch, float* d_snrs, size_t snr_stride,
+                                 void* d_workspace, size_t workspace_bytes, void* stream);
 
 /* Device error flag of a plan: the cone kernel refuses (and leaves unwritten)
  * any work unit that breaks its LDS / register budget and raises the plan's

@@ -53,6 +53,8 @@ _SIGNATURES = {
     "rt_plan_grid": (_c_i, [_vp, _vp, _vp]),
     "rt_plan_workspace_bytes": (_c_i, [_vp, _c_sz, _psz]),
     "rt_periodogram_device": (_c_i, [_vp, _vp, _c_sz, _c_sz, _vp, _c_sz, _vp, _c_sz, _vp]),
+    "rt_periodogram_ladder_device": (_c_i, [_vp, _vp, _c_sz, _c_sz, _vp, _c_sz, _vp]),
+    "rt_periodogram_passes_device": (_c_i, [_vp, _c_sz, _vp, _c_sz, _vp, _c_sz, _vp]),
     "rt_plan_check": (_c_i, [_vp, _vp]),
     "rt_deredden_workspace_bytes": (_c_i, [_c_sz, _c_sz, _c_sz, _c_sz, _psz]),
     "rt_deredden_normalise_device": (_c_i, [_vp, _c_sz, _c_sz, _c_sz, _c_sz, _c_sz, _c_i, _c_i, _vp, _c_sz,

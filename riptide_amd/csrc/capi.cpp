@@ -437,16 +437,31 @@ size_t plan_ws_bytes(const rt_plan* P, size_t batch)
     return b;
 }
 
-void run_periodogram(const rt_plan* P, const float* d_data, size_t batch, size_t data_stride, float* d_snrs,
-                     size_t snr_stride, void* ws, size_t ws_bytes, hipStream_t s)
+// Workspace layout: [leaves | ping | pong]
+struct PlanWs {
+    float* leaves;
+    float* ping;
+    float* pong;
+};
+
+PlanWs plan_ws(const rt_plan* P, size_t batch, void* ws, size_t ws_bytes)
 {
     if (ws_bytes < plan_ws_bytes(P, batch)) throw std::invalid_argument("workspace too small");
     char* w = (char*)ws;
-    float* leaves = (float*)w;
+    PlanWs o;
+    o.leaves = (float*)w;
     w += align_up(P->pg.leaf_floats * 4 * batch, 256);
-    float* ping = (float*)w;
+    o.ping = (float*)w;
     w += align_up(P->dp.ex.scratch_floats * 4 * batch, 256);
-    float* pong = (float*)w;
+    o.pong = (float*)w;
+    return o;
+}
+
+// The downsampling ladder of a batch into the workspace's leaf buffer.
+void run_ladder(const rt_plan* P, const float* d_data, size_t batch, size_t data_stride, void* ws, size_t ws_bytes,
+                hipStream_t s)
+{
+    float* const leaves = plan_ws(P, batch, ws, ws_bytes).leaves;
     ProfRec r{};
     const bool prof = g_prof.on;
     if (prof) {
@@ -474,6 +489,16 @@ void run_periodogram(const rt_plan* P, const float* d_data, size_t batch, size_t
         std::lock_guard<std::mutex> lk(g_prof.mu);
         g_prof.rec[1].push_back(r);
     }
+}
+
+// The FFA passes + fused S/N of a batch whose leaf buffer run_ladder filled.
+void run_passes(const rt_plan* P, size_t batch, float* d_snrs, size_t snr_stride, void* ws, size_t ws_bytes,
+                hipStream_t s)
+{
+    const PlanWs W = plan_ws(P, batch, ws, ws_bytes);
+    float* const leaves = W.leaves;
+    float* const ping = W.ping;
+    float* const pong = W.pong;
     ConeArgs a{};
     a.num_widths = (uint32_t)P->widths.size();
     a.widths = P->d_widths;
@@ -486,6 +511,13 @@ void run_periodogram(const rt_plan* P, const float* d_data, size_t batch, size_t
     a.snr_stride = snr_stride;
     a.error_flag = P->d_flag;
     run_cone_launches(P->dp, a, (uint32_t)batch, s);
+}
+
+void run_periodogram(const rt_plan* P, const float* d_data, size_t batch, size_t data_stride, float* d_snrs,
+                     size_t snr_stride, void* ws, size_t ws_bytes, hipStream_t s)
+{
+    run_ladder(P, d_data, batch, data_stride, ws, ws_bytes, s);
+    run_passes(P, batch, d_snrs, snr_stride, ws, ws_bytes, s);
 }
 
 // Dereddening + normalisation (device).  Workspace layout: [lores | rmed | partials]
@@ -999,6 +1031,26 @@ int rt_periodogram_device(const rt_plan* P, const float* d_data, size_t batch, s
     return guarded([&] {
         if (!batch || !P->pg.length) return RT_OK;
         run_periodogram(P, d_data, batch, data_stride, d_snrs, snr_stride, ws, ws_bytes, (hipStream_t)stream);
+        return RT_OK;
+    });
+}
+
+int rt_periodogram_ladder_device(const rt_plan* P, const float* d_data, size_t batch, size_t data_stride, void* ws,
+                                 size_t ws_bytes, void* stream)
+{
+    return guarded([&] {
+        if (!batch || !P->pg.length) return RT_OK;
+        run_ladder(P, d_data, batch, data_stride, ws, ws_bytes, (hipStream_t)stream);
+        return RT_OK;
+    });
+}
+
+int rt_periodogram_passes_device(const rt_plan* P, size_t batch, float* d_snrs, size_t snr_stride, void* ws,
+                                 size_t ws_bytes, void* stream)
+{
+    return guarded([&] {
+        if (!batch || !P->pg.length) return RT_OK;
+        run_passes(P, batch, d_snrs, snr_stride, ws, ws_bytes, (hipStream_t)stream);
         return RT_OK;
     });
 }

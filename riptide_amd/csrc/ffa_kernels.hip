@@ -18,6 +18,32 @@ namespace rt {
 // ---------------------------------------------------------------------------
 // Downsampling ladder (downsample.hpp:44-82; periodogram.hpp:162-168)
 // ---------------------------------------------------------------------------
+// wmin * w[0] + w[1] + ... + w[cnt - 1], added one by one in that order
+// (downsample.hpp:44-82).  The reads go out eight at a time ahead of their
+// additions (a plain loop waited for every LDS read in turn: at f ~ 100 the
+// ladder was bound by that latency); the elements past cnt - 1 of the last
+// group add -0.0, an exact no-op (x + (-0.0) == x).
+__device__ __forceinline__ float window_sum(const float* w, float wmin, uint32_t cnt)
+{
+    float acc = __fmul_rn(wmin, w[0]);
+    uint32_t i = 1;
+    for (; i + 8 <= cnt; i += 8) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = w[i + j];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc = __fadd_rn(acc, v[j]);
+    }
+    if (i < cnt) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = i + j < cnt ? w[i + j] : -0.0f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc = __fadd_rn(acc, v[j]);
+    }
+    return acc;
+}
+
 // One block = up to 256 consecutive outputs of one rung of one trial (fewer for
 // large f, so the block's input span fits the LDS stage).  The span is loaded
 // with coalesced loads, then each thread sums its window from LDS in the
@@ -70,11 +96,7 @@ __global__ __launch_bounds__(256) void downsample_ladder_kernel(
     const float wmax = (float)__dsub_rn(end, (double)imax);
     const float* w = src + (imin - s0);
     const uint32_t cnt = (uint32_t)(imax - imin);
-    float acc = __fmul_rn(wmin, w[0]);
-    for (uint32_t i = 1; i < cnt; ++i)
-        acc = __fadd_rn(acc, w[i]);
-    acc = __fadd_rn(acc, __fmul_rn(wmax, w[cnt]));
-    out[k] = acc;
+    out[k] = __fadd_rn(window_sum(w, wmin, cnt), __fmul_rn(wmax, w[cnt]));
 }
 
 // Fused ladder: one block per input span (and trial) computes the outputs of
@@ -128,10 +150,7 @@ __global__ __launch_bounds__(256) void downsample_fused_kernel(
             const float wmax = (float)__dsub_rn(end, (double)imax);
             const float* w = span + (imin - s0);
             const uint32_t cnt = (uint32_t)(imax - imin);
-            float acc = __fmul_rn(wmin, w[0]);
-            for (uint32_t i = 1; i < cnt; ++i) acc = __fadd_rn(acc, w[i]);
-            acc = __fadd_rn(acc, __fmul_rn(wmax, w[cnt]));
-            o[k] = acc;
+            o[k] = __fadd_rn(window_sum(w, wmin, cnt), __fmul_rn(wmax, w[cnt]));
         }
     }
 }
@@ -715,6 +734,45 @@ __device__ __forceinline__ void write_rows(float* base, float* dummy, const floa
 // lane 63 from lane 0 of the next slot, and bin p - 1 from bin 0.  Half the
 // LDS reads of the pair.
 //
+// A rolled row read with a wave-uniform wrap slot (RT_WRAP_BRANCH): bins
+// j = lane + 64k of the row at roll t read T[(j + t) mod p].  With
+// K = (p - t) >> 6, every lane of slot k < K reads before the wrap point and
+// every lane of slot k > K after it; only slot K straddles it.  One uniform
+// branch on K (SGPR) picks code in which slots below K read base b, slots
+// above K base b - p, and slot K alone selects per lane: 2 VALU per rolled
+// row instead of a compare and a select per slot.  Same LDS words, same
+// results.  A/B knob, off: cone ms per cfg2 trial 8.65 vs 7.79 with it (the
+// compiler linearises the uniform branches and waits for every case's reads
+// at each join, profiles/r03q_ab_*.log).
+#ifndef RT_WRAP_BRANCH
+#define RT_WRAP_BRANCH 0
+#endif
+template <int SMAX, int KC>
+__device__ __forceinline__ void rolled_case(lds_cptr b, lds_cptr w, int ls, int p, float (&x)[SMAX])
+{
+#pragma unroll
+    for (int k = 0; k < SMAX; ++k) {
+        if (k < KC) x[k] = lds_ld(b + 64 * k);
+        else if (k == KC) x[k] = lds_ld((ls >= p - 64 * k ? w : b) + 64 * k);
+        else x[k] = lds_ld(w + 64 * k);
+    }
+}
+template <int SMAX>
+__device__ __forceinline__ void rolled_row(lds_cptr b, int p, int lane, int t, float (&x)[SMAX])
+{
+    lds_cptr w = b - p;
+    asm("" : "+v"(b), "+v"(w));
+    const int ls = lane + t;
+    const int K = (p - t) >> 6;
+    static_assert(SMAX >= 1 && SMAX <= 5, "wrap-slot cases");
+    if (K <= 0) rolled_case<SMAX, 0>(b, w, ls, p, x);
+    else if (SMAX > 1 && K == 1) rolled_case<SMAX, 1>(b, w, ls, p, x);
+    else if (SMAX > 2 && K == 2) rolled_case<SMAX, 2>(b, w, ls, p, x);
+    else if (SMAX > 3 && K == 3) rolled_case<SMAX, 3>(b, w, ls, p, x);
+    else if (SMAX > 4 && K == 4) rolled_case<SMAX, 4>(b, w, ls, p, x);
+    else rolled_case<SMAX, SMAX>(b, w, ls, p, x);   // p - t >= 64 SMAX: no wrap
+}
+
 // Per-row terms from the row's scalars (SGPRs): r0 head row offset, r1..r3
 // the rolled rows' offsets (+ their rolls), t1..t3 the rolls, c1 carried.
 // HEAD false (row B of a kSlotHalf): only the tail term; hs is row A's.
@@ -722,6 +780,37 @@ template <int SMAX, bool TWO, bool HEAD = true>
 __device__ __forceinline__ void row_terms_s(lds_cptr l1, int p, int lane, int r0, int r1, int r2, int r3, int t1,
                                             int t2, int t3, int c1, float (&hs)[SMAX], float (&ts)[SMAX])
 {
+#if RT_WRAP_BRANCH
+    if constexpr (SMAX <= 5) {
+        if constexpr (TWO) {
+            float x1[SMAX], x2[SMAX], x3[SMAX];
+            if constexpr (HEAD) rolled_row<SMAX>(l1 + r1, p, lane, t1, x1);
+            rolled_row<SMAX>(l1 + r2, p, lane, t2, x2);
+            rolled_row<SMAX>(l1 + r3, p, lane, t3, x3);
+#pragma unroll
+            for (int k = 0; k < SMAX; ++k) {
+                if constexpr (HEAD) hs[k] = __fadd_rn(lds_ld(l1 + r0 + 64 * k), x1[k]);
+                ts[k] = __fadd_rn(x2[k], x3[k]);
+            }
+        } else {
+            float x[SMAX];
+            rolled_row<SMAX>(l1 + r1, p, lane, t1, x);
+            if constexpr (HEAD) {
+                const uint32_t keep = c1 ? 0u : 0xFFFFFFFFu;
+                const uint32_t neg0 = ~keep & 0x80000000u;
+#pragma unroll
+                for (int k = 0; k < SMAX; ++k) {
+                    hs[k] = lds_ld(l1 + r0 + 64 * k);
+                    ts[k] = __uint_as_float((__float_as_uint(x[k]) & keep) | neg0);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < SMAX; ++k) ts[k] = x[k];
+            }
+        }
+        return;
+    }
+#endif
     if constexpr (TWO && !HEAD) {
         lds_cptr b2 = l1 + r2;
         lds_cptr b3 = l1 + r3;
@@ -2281,6 +2370,29 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
 // WIDE: final units whose S/N takes the widths past its register window as
 // plain LDS windows (snr_wide_ok; a separate instantiation, so the plans
 // without such widths run code without it)
+// XCD-aware unit order: workgroups are dealt round-robin over the 8 XCDs
+// (blocks b and b + 8 share one, MI355X_MICROARCH.md "Workgroup dispatch"),
+// so with u = blockIdx.x the batch's trials of one item -- which read the
+// same unit record, blob and DMA segment table -- were spread over all 8
+// L2s.  Here the units of an item (u = item * batch + trial) go to one XCD:
+// XCD x takes items x, x + 8, ... in order, its blocks b = 8 i + x running
+// unit (8 (i / batch) + x) * batch + i % batch.  A bijection on the first
+// 8 * batch * floor(total / (8 * batch)) units, identity on the rest; the
+// global longest-first order is kept per XCD.  A/B knob, off: same box, cone
+// ms per trial cfg2 7.87 vs 7.79, cfg3 1.951 vs 1.924, cfg4 0.883 vs 0.871
+// with it (profiles/r03q_ab_*.log).
+#ifndef RT_XCD_MAP
+#define RT_XCD_MAP 0
+#endif
+__device__ __forceinline__ uint32_t xcd_unit(uint32_t b, uint32_t total, uint32_t batch)
+{
+    if (!RT_XCD_MAP || batch < 2) return b;
+    const uint32_t span = 8u * batch;
+    if (b >= total / span * span) return b;
+    const uint32_t i = b >> 3, x = b & 7u;
+    return ((i / batch) * 8u + x) * batch + i % batch;
+}
+
 template <int SMAX, int RWT = 0, bool WIDE = false>
 __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(ConeArgs a)
 {
@@ -2304,8 +2416,8 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
     unsigned long long t_begin[3] = {};
 #endif
     const uint32_t total = a.num_items * a.batch;
-    uint32_t u = blockIdx.x;
-    if (u >= total) return;
+    if (blockIdx.x >= total) return;
+    uint32_t u = kConeBuffers == 1 ? xcd_unit(blockIdx.x, total, a.batch) : blockIdx.x;
     if (tid < (int)a.num_widths) wl[tid] = (int)a.widths[tid];   // visible after the first barrier
     if (tid == 0) {
         uint32_t wm = 0;

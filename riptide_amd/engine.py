@@ -108,6 +108,45 @@ class PeriodogramPlan:
             self.check(s)
         return out[0] if squeeze else out
 
+    def _ws_ok(self, workspace, B):
+        import torch
+        need = self.workspace_bytes(B)
+        if (workspace is None or workspace.dtype != torch.uint8 or workspace.device != self.device
+                or not workspace.is_contiguous() or workspace.numel() < need):
+            raise ValueError(f"workspace must be a contiguous uint8 tensor of >= {need} bytes on the plan's device")
+
+    def ladder(self, data, workspace, stream=None):
+        """First half of run(): the downsampling ladder of data float32 [B, size]
+        into `workspace`'s leaf buffer (rt_periodogram_ladder_device).  With
+        passes() on another stream, batch k + 1's ladder overlaps batch k's
+        FFA passes; the caller orders the two halves of one batch (an event)
+        and keeps a workspace per batch in flight."""
+        import torch
+        if data.dim() != 2 or data.dtype != torch.float32 or data.device != self.device or data.shape[1] != self.size:
+            raise ValueError("data must be float32 [B, size] on the plan's device")
+        if data.stride(1) != 1:
+            raise ValueError("data rows must be contiguous")
+        B = data.shape[0]
+        self._ws_ok(workspace, B)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _check(_L.rt_periodogram_ladder_device(self._h, _lib.ptr(data), B, data.stride(0), _lib.ptr(workspace),
+                                               workspace.numel(), _stream_handle(s)))
+
+    def passes(self, out, workspace, stream=None):
+        """Second half of run(): FFA passes + fused S/N of the batch whose
+        ladder filled `workspace`, into out float32 [B, L, W]."""
+        import torch
+        B = out.shape[0]
+        if (out.dtype != torch.float32 or out.device != self.device or not out.is_contiguous()
+                or tuple(out.shape) != (B, self.length, self.num_widths)):
+            raise ValueError(f"out must be a contiguous float32 [B, {self.length}, {self.num_widths}] "
+                             "tensor on the plan's device")
+        self._ws_ok(workspace, B)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _check(_L.rt_periodogram_passes_device(self._h, B, _lib.ptr(out), self.length * self.num_widths,
+                                               _lib.ptr(workspace), workspace.numel(), _stream_handle(s)))
+        return out
+
     def check(self, stream=None):
         """Raise EngineError if any cone work unit of the runs since the last
         check broke its LDS / register budget (its S/N rows were left
