@@ -131,6 +131,16 @@ constexpr int kSlotWords = kConeWgsPerCu == 4 ? 288 : 544;   // LDS area of a un
 // single steps) and the slot word
 RT_HD constexpr bool resolved_slots(int smax) { return smax == 4 || smax == 5; }
 constexpr int kAuxMetaWords = kBlobHeader + kDescEntries + kMaxRows + kSlotWords;   // the metadata area
+// 4-slot roll table (ffa_kernels.hip row_terms_lut): 2 words per entry
+// x < 256 + 64 at the end of the metadata area, which it extends by kLutPad
+// words (the workgroup's LDS stays inside the same 512-byte granule); every
+// 4-slot row-slot unit's blob LDS part must end at or before kLut4Off
+#ifndef RT_ROLL_LUT
+#define RT_ROLL_LUT 1
+#endif
+constexpr int kLutPad = 64;
+constexpr int kLut4Words = 2 * (256 + 64);
+constexpr int kLut4Off = kAuxMetaWords + kLutPad - kLut4Words;
 constexpr uint32_t kNoBlob = 0xFFFFFFFFu;
 constexpr uint32_t kCarriedRow = 1023;
 // 16-byte chunks of a unit's LDS DMA fill (setup_unit): a whole unit's block

@@ -280,6 +280,7 @@ __device__ __forceinline__ UnitView unit_view(const ConeArgs& a, int item, int t
 // blob (kBlobHeader words of header, the DMA runs, the descriptor table, the
 // bottom-row offsets) DMA'd into `aux`.
 constexpr int kAuxWords = kBlobHeader + kDescEntries + kMaxRows + kSlotWords;
+static_assert(kAuxWords == kAuxMetaWords, "metadata area");
 struct UnitCtx {
     UnitView U;
     bool tile;                // a tile unit (else: a whole node)
@@ -288,6 +289,7 @@ struct UnitCtx {
     bool slots;               // the blob holds row-slot tables (merge_step_slots)
     int nruns, entries, nb;   // blob header counts
     const uint32_t* aux;      // the blob's LDS part in LDS
+    const uint32_t* aux0;     // the workgroup's metadata area (roll table at kLut4Off)
 };
 
 __device__ __forceinline__ int rows_at(const UnitCtx& C, int l)
@@ -351,6 +353,7 @@ __device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t u, uin
     C.tile = U.mode == kModeTile;
     C.table = U.blob != kNoBlob;
     C.aux = aux;
+    C.aux0 = aux;
     const int p = U.p;
     const int slots = merge_slots((uint32_t)p);
     ok = U.levels <= kMaxLevels && p > 0 &&
@@ -392,6 +395,8 @@ __device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t u, uin
                  C.nb * pack_stride(p) + words <= kLdsBufFloats;
         } else {
             ok = ok && C.nb <= cap && C.entries <= kDescEntries && words <= kAuxWords;
+            // the 4-slot roll table lies past the blob's LDS part
+            if (SMAX == 4 && RT_ROLL_LUT && C.slots) ok = ok && words <= kLut4Off;
         }
         ok = ok && words >= kBlobHeader + C.entries + C.nb && C.nruns <= 64 * kConeWaves && (words & 3) == 0;
 #ifdef RT_STAMPS
@@ -871,12 +876,130 @@ __device__ __forceinline__ void row_terms_s(lds_cptr l1, int p, int lane, int r0
     }
 }
 
+// Roll table (RT_ROLL_LUT, 4-slot rows, p = 193..256): a rolled read of a
+// row at roll t takes bin j = lane + 64k from T[(lane + t + 64k) mod p].
+// Entry x = lane + t (x < p + 64) of a per-unit LDS table holds the four
+// byte offsets 4 ((x + 64k) mod p), k = 0..3, as 16-bit halves of 8 bytes:
+// one conflict-free ds_read_b64 per rolled row (consecutive lanes,
+// consecutive entries), then one address add per slot from the row's start
+// (an SGPR) -- instead of a compare and a select per slot against the wrap
+// point.  Same LDS words, same additions: bit-exact.  The table sits at the
+// end of the unit's metadata area (kLut4Off, past every blob's LDS part:
+// validate_exec_plan) and is rebuilt by every unit of a 4-slot instance.
+typedef const __attribute__((address_space(3))) unsigned long long* lut_cptr;
+typedef const __attribute__((address_space(3))) char* lds_ccptr;
+
+// rolled row whose roll-table entry is e and whose row starts at byte `rb`
+// of LDS (uniform)
+__device__ __forceinline__ void rolled_lut4(lds_ccptr rb, unsigned long long e, float (&x)[4])
+{
+    const uint32_t e0 = (uint32_t)e, e1 = (uint32_t)(e >> 32);
+    x[0] = lds_ld((lds_cptr)(rb + (e0 & 0xFFFFu)));
+    x[1] = lds_ld((lds_cptr)(rb + (e0 >> 16)));
+    x[2] = lds_ld((lds_cptr)(rb + (e1 & 0xFFFFu)));
+    x[3] = lds_ld((lds_cptr)(rb + (e1 >> 16)));
+}
+
+// row_terms_s with the roll table: s0 the level's rows (uniform), r0 the head
+// row's offset, q1..q3 the rolled rows' offsets WITHOUT their rolls t1..t3.
+// The table entries are read first (plain loads, free to move) and the head
+// row before the rolled rows (the volatile reads keep their order), so the
+// head reads are in flight while the entries return.
+template <bool TWO, bool HEAD = true>
+__device__ __forceinline__ void row_terms_lut(lds_cptr l1, lds_cptr s0, lut_cptr lutl, int r0, int q1, int q2, int q3,
+                                              int t1, int t2, int t3, int c1, float (&hs)[4], float (&ts)[4])
+{
+    const lds_ccptr b = (lds_ccptr)s0;
+    if constexpr (TWO) {
+        const unsigned long long e1 = HEAD ? lutl[t1] : 0ull, e2 = lutl[t2], e3 = lutl[t3];
+        float h[4], x1[4], x2[4], x3[4];
+        if constexpr (HEAD) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) h[k] = lds_ld(l1 + r0 + 64 * k);
+            rolled_lut4(b + 4 * q1, e1, x1);
+        }
+        rolled_lut4(b + 4 * q2, e2, x2);
+        rolled_lut4(b + 4 * q3, e3, x3);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if constexpr (HEAD) hs[k] = __fadd_rn(h[k], x1[k]);
+            ts[k] = __fadd_rn(x2[k], x3[k]);
+        }
+    } else {
+        const unsigned long long e = lutl[t1];
+        float x[4];
+        if constexpr (HEAD) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) hs[k] = lds_ld(l1 + r0 + 64 * k);
+        }
+        rolled_lut4(b + 4 * q1, e, x);
+        if constexpr (HEAD) {
+            // c1: a carried size-1 node (its tail term is -0.0, x + (-0.0) == x)
+            const uint32_t keep = c1 ? 0u : 0xFFFFFFFFu;
+            const uint32_t neg0 = ~keep & 0x80000000u;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ts[k] = __uint_as_float((__float_as_uint(x[k]) & keep) | neg0);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ts[k] = x[k];
+        }
+    }
+}
+
+// Builds the roll table of rows of p bins (4-slot instances) at `lut`:
+// entry x < p + 64 = {4 (x mod p) | 4 ((x + 64) mod p) << 16,
+//                     4 ((x + 128) mod p) | 4 ((x + 192) mod p) << 16}.
+__device__ __forceinline__ void build_roll_lut4(uint32_t* lut, int p, int tid)
+{
+    for (int w = tid; w < 2 * (p + 64); w += kConeBlock) {
+        const int x = (w >> 1) + 128 * (w & 1);
+        int y0 = x, y1 = x + 64;
+        // y < p + 256 < 3p (p >= 193): at most two subtractions
+        y0 -= y0 >= p ? p : 0;
+        y0 -= y0 >= p ? p : 0;
+        y1 -= y1 >= p ? p : 0;
+        y1 -= y1 >= p ? p : 0;
+        lut[w] = (uint32_t)(4 * y0) | ((uint32_t)(4 * y1) << 16);
+    }
+}
+
 // Per-row terms of the row whose resolved descriptor sits in lane i
 // (unpacked per lane: o0 .. o3, s1 .. s3; seven v_readlane per row).
 template <int SMAX, bool TWO, bool HEAD = true>
 __device__ __forceinline__ void row_terms(lds_cptr l1, int p, int lane, int i, int o0, int o1, int o2, int o3, int s1,
-                                          int s2, int s3, float (&hs)[SMAX], float (&ts)[SMAX])
+                                          int s2, int s3, float (&hs)[SMAX], float (&ts)[SMAX],
+                                          lds_cptr s0 = nullptr, lut_cptr lutl = nullptr)
 {
+    if constexpr (SMAX == 4 && RT_ROLL_LUT) {
+        // o1 .. o3 are the rolled rows' offsets without their rolls here
+        if constexpr (TWO) {
+            if constexpr (HEAD) {
+                int r0 = __builtin_amdgcn_readlane(o0, i), q1 = __builtin_amdgcn_readlane(o1, i);
+                int q2 = __builtin_amdgcn_readlane(o2, i), q3 = __builtin_amdgcn_readlane(o3, i);
+                int t1 = __builtin_amdgcn_readlane(s1, i), t2 = __builtin_amdgcn_readlane(s2, i);
+                int t3 = __builtin_amdgcn_readlane(s3, i);
+                asm volatile("" : "+s"(r0), "+s"(q1), "+s"(q2), "+s"(q3), "+s"(t1), "+s"(t2), "+s"(t3));
+                row_terms_lut<true>(l1, s0, lutl, r0, q1, q2, q3, t1, t2, t3, 0, hs, ts);
+            } else {
+                int q2 = __builtin_amdgcn_readlane(o2, i), q3 = __builtin_amdgcn_readlane(o3, i);
+                int t2 = __builtin_amdgcn_readlane(s2, i), t3 = __builtin_amdgcn_readlane(s3, i);
+                asm volatile("" : "+s"(q2), "+s"(q3), "+s"(t2), "+s"(t3));
+                row_terms_lut<true, false>(l1, s0, lutl, 0, 0, q2, q3, 0, t2, t3, 0, hs, ts);
+            }
+        } else {
+            if constexpr (HEAD) {
+                int r0 = __builtin_amdgcn_readlane(o0, i), q1 = __builtin_amdgcn_readlane(o1, i);
+                int t1 = __builtin_amdgcn_readlane(s1, i), c1 = __builtin_amdgcn_readlane(o2, i);
+                asm volatile("" : "+s"(r0), "+s"(q1), "+s"(t1), "+s"(c1));
+                row_terms_lut<false>(l1, s0, lutl, r0, q1, 0, 0, t1, 0, 0, c1, hs, ts);
+            } else {
+                int q1 = __builtin_amdgcn_readlane(o1, i), t1 = __builtin_amdgcn_readlane(s1, i);
+                asm volatile("" : "+s"(q1), "+s"(t1));
+                row_terms_lut<false, false>(l1, s0, lutl, 0, q1, 0, 0, t1, 0, 0, 0, hs, ts);
+            }
+        }
+        return;
+    }
     // all of the row's scalars first, in distinct SGPRs: a v_readlane result
     // read by the next VALU instruction costs s_nop wait states
     if constexpr (TWO) {
@@ -965,16 +1088,18 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
         ey = e.y;
         ez = e.z;
         s1 = (int)(e.z & 1023u);
+        // the roll table path takes the rolled rows' offsets without rolls
+        constexpr int roll_in = SMAX == 4 && RT_ROLL_LUT ? 0 : 1;
         if constexpr (TWO) {
             s2 = (int)((e.z >> 10) & 1023u);
             s3 = (int)((e.z >> 20) & 1023u);
             o0 = (int)(e.x & 0xFFFFu);
-            o1 = (int)(e.x >> 16) + s1;
-            o2 = (int)(e.y & 0xFFFFu) + s2;
-            o3 = (int)(e.y >> 16) + s3;
+            o1 = (int)(e.x >> 16) + roll_in * s1;
+            o2 = (int)(e.y & 0xFFFFu) + roll_in * s2;
+            o3 = (int)(e.y >> 16) + roll_in * s3;
         } else {
             o0 = (int)(e.x & 0xFFFFu);
-            o1 = (int)(e.x >> 16) + s1;
+            o1 = (int)(e.x >> 16) + roll_in * s1;
             o2 = (int)((e.z >> 30) & 1u);
         }
         (void)loff;
@@ -1013,6 +1138,8 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
     }
     }
     const lds_cptr l1 = (lds_cptr)src + lane;
+    const lds_cptr s0 = (lds_cptr)src;
+    const lut_cptr lutl = (lut_cptr)(C.aux0 + kLut4Off) + lane;
     const int jl = p - 1 - 64 * (SMAX - 1);   // lane of bin p - 1 in the last slot
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
@@ -1022,7 +1149,7 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
             if constexpr (resolved_slots(SMAX) && RT_PACKED_READLANE)
                 row_terms_packed<SMAX, TWO>(l1, p, lane, q, ex, ey, ez, hs, ts);
             else
-                row_terms<SMAX, TWO>(l1, p, lane, q, o0, o1, o2, o3, s1, s2, s3, hs, ts);
+                row_terms<SMAX, TWO>(l1, p, lane, q, o0, o1, o2, o3, s1, s2, s3, hs, ts, s0, lutl);
 #pragma unroll
             for (int k = 0; k < SMAX; ++k) v[2 * q][k] = __fadd_rn(hs[k], ts[k]);
             const int qb = 2 * q + 1 < RW ? 2 * q + 1 : RW - 1;   // row B's register row (q < Q: in range)
@@ -1041,14 +1168,14 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
                 } else if (kq == kSlotHalf) {
                     // row B shares row A's head term: only its tail term
                     float tb[SMAX];
-                    row_terms<SMAX, TWO, false>(l1, p, lane, 32 + q, o0, o1, o2, o3, s1, s2, s3, hs, tb);
+                    row_terms<SMAX, TWO, false>(l1, p, lane, 32 + q, o0, o1, o2, o3, s1, s2, s3, hs, tb, s0, lutl);
 #pragma unroll
                     for (int k = 0; k < SMAX; ++k) v[qb][k] = __fadd_rn(hs[k], tb[k]);
                 } else if (kq == kSlotTwo) {
                     if constexpr (resolved_slots(SMAX) && RT_PACKED_READLANE)
                         row_terms_packed<SMAX, TWO>(l1, p, lane, 32 + q, ex, ey, ez, hs, ts);
                     else
-                        row_terms<SMAX, TWO>(l1, p, lane, 32 + q, o0, o1, o2, o3, s1, s2, s3, hs, ts);
+                        row_terms<SMAX, TWO>(l1, p, lane, 32 + q, o0, o1, o2, o3, s1, s2, s3, hs, ts, s0, lutl);
 #pragma unroll
                     for (int k = 0; k < SMAX; ++k) v[qb][k] = __fadd_rn(hs[k], ts[k]);
                 }
@@ -1286,10 +1413,46 @@ __device__ __forceinline__ void pack_rolled(lds_cptr sp, int o, int j0, int s, i
     for (int e = 0; e < kPackSeg; ++e) x[e] = lds_ld((e >= w ? hi : lo) + e);
 }
 
+// The same from the short-row roll table (RT_PACK_LUT): entry x = j0 + s
+// (x < 2p <= 64) holds the byte offsets 4 ((x + e) mod p) of the segment's
+// eight elements as bytes: one conflict-free ds_read_b64 per rolled segment,
+// then one address add per element (byte select) instead of a compare and a
+// select.  Same LDS words: bit-exact.  The table lives in the metadata area,
+// which short-row units do not use (their blob is in their level buffer).
+#ifndef RT_PACK_LUT
+#define RT_PACK_LUT 1
+#endif
+__device__ __forceinline__ void pack_rolled_lut(lds_cptr sp, int o, unsigned long long e, float (&x)[kPackSeg])
+{
+    const lds_ccptr rb = (lds_ccptr)(sp + o);
+    const uint32_t e0 = (uint32_t)e, e1 = (uint32_t)(e >> 32);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = lds_ld((lds_cptr)(rb + ((e0 >> (8 * k)) & 0xFFu)));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[4 + k] = lds_ld((lds_cptr)(rb + ((e1 >> (8 * k)) & 0xFFu)));
+}
+
+__device__ __forceinline__ void build_pack_lut(uint32_t* lut, int p, int tid)
+{
+    for (int w = tid; w < 4 * p; w += kConeBlock) {
+        const int x = (w >> 1) + 4 * (w & 1);
+        uint32_t word = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            int y = x + i;                        // < 2p + 8 <= 3p (p >= 8)
+            y -= y >= p ? p : 0;
+            y -= y >= p ? p : 0;
+            word |= (uint32_t)(4 * y) << (8 * i);
+        }
+        lut[w] = word;
+    }
+}
+
 template <bool TWO, bool FIRST>
 __device__ __forceinline__ void merge_step_tasks(const UnitCtx& C, const float* src, int p, int qs, int lo, int tid,
                                                  int nrows, float (&v)[kPackTasks][kPackSeg], const int* loff)
 {
+    const lut_cptr plut = (lut_cptr)C.aux0;
     const int segs = pack_segments(p);
     const int ntask = nrows * segs;
     const uint32_t* const desc = desc_table(C);
@@ -1316,11 +1479,21 @@ __device__ __forceinline__ void merge_step_tasks(const UnitCtx& C, const float* 
                 const int o3 = FIRST ? loff[q3] : (int)__umul24(q3, (uint32_t)qs);
                 float x2[kPackSeg], x3[kPackSeg];
                 const lds_cptr h0 = sp + o0 + j0;
+                if (RT_PACK_LUT) {
+                    // table entries first (plain loads), then the volatile reads
+                    const unsigned long long e1 = plut[j0 + sH], e2 = plut[j0 + sh], e3 = plut[j0 + sTT];
 #pragma unroll
-                for (int k = 0; k < kPackSeg; ++k) x0[k] = lds_ld(h0 + k);
-                pack_rolled(sp, o1, j0, sH, p, x1);
-                pack_rolled(sp, o2, j0, sh, p, x2);
-                pack_rolled(sp, o3, j0, sTT, p, x3);
+                    for (int k = 0; k < kPackSeg; ++k) x0[k] = lds_ld(h0 + k);
+                    pack_rolled_lut(sp, o1, e1, x1);
+                    pack_rolled_lut(sp, o2, e2, x2);
+                    pack_rolled_lut(sp, o3, e3, x3);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < kPackSeg; ++k) x0[k] = lds_ld(h0 + k);
+                    pack_rolled(sp, o1, j0, sH, p, x1);
+                    pack_rolled(sp, o2, j0, sh, p, x2);
+                    pack_rolled(sp, o3, j0, sTT, p, x3);
+                }
 #pragma unroll
                 for (int k = 0; k < kPackSeg; ++k) v[i][k] = __fadd_rn(__fadd_rn(x0[k], x1[k]), __fadd_rn(x2[k], x3[k]));
             } else {
@@ -1331,9 +1504,16 @@ __device__ __forceinline__ void merge_step_tasks(const UnitCtx& C, const float* 
                 const int ho = FIRST ? loff[d & 1023u] : (int)__umul24(d & 1023u, (uint32_t)qs);
                 const int to = car ? ho : (FIRST ? loff[tc & 1023u] : (int)__umul24(tc, (uint32_t)qs));
                 const lds_cptr h0 = sp + ho + j0;
+                if (RT_PACK_LUT) {
+                    const unsigned long long e1 = plut[j0 + (car ? 0 : sh)];
 #pragma unroll
-                for (int k = 0; k < kPackSeg; ++k) x0[k] = lds_ld(h0 + k);
-                pack_rolled(sp, to, j0, car ? 0 : sh, p, x1);
+                    for (int k = 0; k < kPackSeg; ++k) x0[k] = lds_ld(h0 + k);
+                    pack_rolled_lut(sp, to, e1, x1);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < kPackSeg; ++k) x0[k] = lds_ld(h0 + k);
+                    pack_rolled(sp, to, j0, car ? 0 : sh, p, x1);
+                }
                 // a carried size-1 node adds -0.0 (x + (-0.0) == x: the reference's copy)
 #pragma unroll
                 for (int k = 0; k < kPackSeg; ++k) v[i][k] = __fadd_rn(x0[k], car ? -0.0f : x1[k]);
@@ -2398,7 +2578,7 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
 {
     constexpr int RW = RWT ? RWT : merge_rows_per_wave(SMAX);   // register rows per wave
     __shared__ __attribute__((aligned(16))) float data[kConeBuffers][kLdsBufFloats + kLdsPadFloats];
-    __shared__ __attribute__((aligned(16))) uint32_t aux[kConeBuffers][kAuxWords];   // tile units: the host blob
+    __shared__ __attribute__((aligned(16))) uint32_t aux[kConeBuffers][kAuxWords + kLutPad];   // the host blob (+ roll table)
     // boxcar widths (LDS reads never wait on the S/N stores in flight), then
     // the widest of them
     __shared__ int wl[kMaxWidths + 1];
@@ -2446,6 +2626,13 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
         // below (the S/N row passes have no barrier of their own)
         if (U.dst == kSelSnr && tid < (int)a.num_widths) snr_width_consts(wl[tid], p, whb + 2 * tid);
 #endif
+        // the roll table of a 4-slot unit (past its blob's LDS part, which
+        // the DMA may still be writing), published by the barrier below
+        if constexpr (SMAX == 4 && RT_ROLL_LUT)
+            if (C.slots && ok) build_roll_lut4(aux[b] + kLut4Off, p, tid);
+        // the short-row roll table (RT_PACK_LUT) in the unused metadata area
+        if constexpr (SMAX == kPack2 && RT_PACK_LUT)
+            if (ok && p >= kPackSeg) build_pack_lut(aux[b], p, tid);
         // every wave waits for its own DMA (the previous unit's stores count
         // in the same in-order counter), the barrier publishes all of them
         __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)

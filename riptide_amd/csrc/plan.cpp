@@ -786,6 +786,9 @@ static void validate_blob(const ConeItem& it, uint32_t p, int smax, int rw, cons
     if (runoff < (uint32_t)kBlobHeader + entries + nb + slot_words || (runoff & 3u) || nb != w[kHdrRows + L])
         throw std::runtime_error("schedule: malformed unit blob header");
     if (4 * fill > (uint32_t)kLdsBufFloats) throw std::runtime_error("schedule: unit fill exceeds the LDS level buffer");
+    // a 4-slot row-slot unit's roll table follows its blob's LDS part
+    if (RT_ROLL_LUT && smax == 4 && slot_words && runoff > (uint32_t)kLut4Off)
+        throw std::runtime_error("schedule: unit blob overlaps the roll table");
     uint32_t c = 0;
     const uint32_t K = (nseg + kConeWaves - 1) / kConeWaves;   // wave-major segment order
     for (uint32_t i = 0; i < nseg; ++i) {
