@@ -886,6 +886,13 @@ __device__ __forceinline__ void row_terms_s(lds_cptr l1, int p, int lane, int r0
 // point.  Same LDS words, same additions: bit-exact.  The table sits at the
 // end of the unit's metadata area (kLut4Off, past every blob's LDS part:
 // validate_exec_plan) and is rebuilt by every unit of a 4-slot instance.
+// roll-table entries of row A read one slot ahead (merge_step_slots).  A/B
+// knob, off: neutral (cone ms per trial cfg2 7.69 / 7.68 with it vs 7.70 /
+// 7.68, profiles/r03w_ab_*.log) -- the table's round trip was not on the
+// critical path
+#ifndef RT_LUT_AHEAD
+#define RT_LUT_AHEAD 0
+#endif
 typedef const __attribute__((address_space(3))) unsigned long long* lut_cptr;
 typedef const __attribute__((address_space(3))) char* lds_ccptr;
 
@@ -907,11 +914,14 @@ __device__ __forceinline__ void rolled_lut4(lds_ccptr rb, unsigned long long e, 
 // head reads are in flight while the entries return.
 template <bool TWO, bool HEAD = true>
 __device__ __forceinline__ void row_terms_lut(lds_cptr l1, lds_cptr s0, lut_cptr lutl, int r0, int q1, int q2, int q3,
-                                              int t1, int t2, int t3, int c1, float (&hs)[4], float (&ts)[4])
+                                              int t1, int t2, int t3, int c1, float (&hs)[4], float (&ts)[4],
+                                              const unsigned long long* pre = nullptr)
 {
     const lds_ccptr b = (lds_ccptr)s0;
     if constexpr (TWO) {
-        const unsigned long long e1 = HEAD ? lutl[t1] : 0ull, e2 = lutl[t2], e3 = lutl[t3];
+        // pre: the row's three entries, read one slot ahead (merge_step_slots)
+        const unsigned long long e1 = pre ? pre[0] : (HEAD ? lutl[t1] : 0ull);
+        const unsigned long long e2 = pre ? pre[1] : lutl[t2], e3 = pre ? pre[2] : lutl[t3];
         float h[4], x1[4], x2[4], x3[4];
         if constexpr (HEAD) {
 #pragma unroll
@@ -926,7 +936,7 @@ __device__ __forceinline__ void row_terms_lut(lds_cptr l1, lds_cptr s0, lut_cptr
             ts[k] = __fadd_rn(x2[k], x3[k]);
         }
     } else {
-        const unsigned long long e = lutl[t1];
+        const unsigned long long e = pre ? pre[0] : lutl[t1];
         float x[4];
         if constexpr (HEAD) {
 #pragma unroll
@@ -968,7 +978,8 @@ __device__ __forceinline__ void build_roll_lut4(uint32_t* lut, int p, int tid)
 template <int SMAX, bool TWO, bool HEAD = true>
 __device__ __forceinline__ void row_terms(lds_cptr l1, int p, int lane, int i, int o0, int o1, int o2, int o3, int s1,
                                           int s2, int s3, float (&hs)[SMAX], float (&ts)[SMAX],
-                                          lds_cptr s0 = nullptr, lut_cptr lutl = nullptr)
+                                          lds_cptr s0 = nullptr, lut_cptr lutl = nullptr,
+                                          const unsigned long long* pre = nullptr)
 {
     if constexpr (SMAX == 4 && RT_ROLL_LUT) {
         // o1 .. o3 are the rolled rows' offsets without their rolls here
@@ -979,7 +990,7 @@ __device__ __forceinline__ void row_terms(lds_cptr l1, int p, int lane, int i, i
                 int t1 = __builtin_amdgcn_readlane(s1, i), t2 = __builtin_amdgcn_readlane(s2, i);
                 int t3 = __builtin_amdgcn_readlane(s3, i);
                 asm volatile("" : "+s"(r0), "+s"(q1), "+s"(q2), "+s"(q3), "+s"(t1), "+s"(t2), "+s"(t3));
-                row_terms_lut<true>(l1, s0, lutl, r0, q1, q2, q3, t1, t2, t3, 0, hs, ts);
+                row_terms_lut<true>(l1, s0, lutl, r0, q1, q2, q3, t1, t2, t3, 0, hs, ts, pre);
             } else {
                 int q2 = __builtin_amdgcn_readlane(o2, i), q3 = __builtin_amdgcn_readlane(o3, i);
                 int t2 = __builtin_amdgcn_readlane(s2, i), t3 = __builtin_amdgcn_readlane(s3, i);
@@ -991,7 +1002,7 @@ __device__ __forceinline__ void row_terms(lds_cptr l1, int p, int lane, int i, i
                 int r0 = __builtin_amdgcn_readlane(o0, i), q1 = __builtin_amdgcn_readlane(o1, i);
                 int t1 = __builtin_amdgcn_readlane(s1, i), c1 = __builtin_amdgcn_readlane(o2, i);
                 asm volatile("" : "+s"(r0), "+s"(q1), "+s"(t1), "+s"(c1));
-                row_terms_lut<false>(l1, s0, lutl, r0, q1, 0, 0, t1, 0, 0, c1, hs, ts);
+                row_terms_lut<false>(l1, s0, lutl, r0, q1, 0, 0, t1, 0, 0, c1, hs, ts, pre);
             } else {
                 int q1 = __builtin_amdgcn_readlane(o1, i), t1 = __builtin_amdgcn_readlane(s1, i);
                 asm volatile("" : "+s"(q1), "+s"(t1));
@@ -1141,15 +1152,33 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
     const lds_cptr s0 = (lds_cptr)src;
     const lut_cptr lutl = (lut_cptr)(C.aux0 + kLut4Off) + lane;
     const int jl = p - 1 - 64 * (SMAX - 1);   // lane of bin p - 1 in the last slot
+    // roll table: row A's table entries are read one slot ahead (their LDS
+    // round trip overlaps the previous slot's reads); slots past nq read
+    // valid entries of their lanes' clamped rows and are never used
+    constexpr bool PRE = SMAX == 4 && RT_ROLL_LUT && RT_LUT_AHEAD;
+    unsigned long long pe[3] = {0ull, 0ull, 0ull};
+    auto lut_ahead = [&](int q) {
+        if constexpr (PRE) {
+            pe[0] = lutl[__builtin_amdgcn_readlane(s1, q)];
+            if constexpr (TWO) {
+                pe[1] = lutl[__builtin_amdgcn_readlane(s2, q)];
+                pe[2] = lutl[__builtin_amdgcn_readlane(s3, q)];
+            }
+        }
+    };
+    lut_ahead(0);
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
         if (q < nq) {
             const uint32_t kq = (uint32_t)__builtin_amdgcn_readlane((int)sw, q) >> 20;
             float hs[SMAX], ts[SMAX];
-            if constexpr (resolved_slots(SMAX) && RT_PACKED_READLANE)
+            if constexpr (resolved_slots(SMAX) && RT_PACKED_READLANE) {
                 row_terms_packed<SMAX, TWO>(l1, p, lane, q, ex, ey, ez, hs, ts);
-            else
-                row_terms<SMAX, TWO>(l1, p, lane, q, o0, o1, o2, o3, s1, s2, s3, hs, ts, s0, lutl);
+            } else {
+                unsigned long long cur[3] = {pe[0], pe[1], pe[2]};
+                if (q + 1 < Q) lut_ahead(q + 1);
+                row_terms<SMAX, TWO>(l1, p, lane, q, o0, o1, o2, o3, s1, s2, s3, hs, ts, s0, lutl, PRE ? cur : nullptr);
+            }
 #pragma unroll
             for (int k = 0; k < SMAX; ++k) v[2 * q][k] = __fadd_rn(hs[k], ts[k]);
             const int qb = 2 * q + 1 < RW ? 2 * q + 1 : RW - 1;   // row B's register row (q < Q: in range)
@@ -2032,6 +2061,13 @@ __device__ __forceinline__ float grp_allmax(float v)
 #ifndef RT_SNR_WAVE_LOCAL
 #define RT_SNR_WAVE_LOCAL 1
 #endif
+// S/N column masks from two wave-uniform lane masks (snr_rows col_ok).  A/B
+// knob, off: 17 fewer v_cmp per row pass, but cone ms per trial cfg2 7.76 vs
+// 7.68, cfg3 1.92 vs 1.91 with it (the SALU mask selects feed every column's
+// v_cndmask through VCC; profiles/r03v_ab_*.log)
+#ifndef RT_SNR_SMASK
+#define RT_SNR_SMASK 0
+#endif
 
 // NR rows per lane and pass (NR = 2: the lane's rows r and r + 512/G are
 // independent chains interleaved in one instruction stream, and half as many
@@ -2065,6 +2101,18 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
     const bool unmasked = zpad && natural && c == CH;
     int cnt = max(min(j0 + c, p) - j0, 0);        // columns of this lane (may be 0)
     const int owner = (p - 1) / c;
+    // Column masks as wave-uniform lane masks: a row's lanes hold c columns
+    // each except lane p / c, which holds p mod c (the later lanes none), so
+    // column i is valid in the lanes of m_any (i < p mod c), of m_full
+    // (p mod c <= i < c) or in none; the same for every row of the wave.  A
+    // column select is then one v_cndmask with an SGPR mask instead of a
+    // v_cmp against the lane's count and a v_cndmask.
+    const int cpart = uni(p % c);
+    const uint64_t m_any = __builtin_amdgcn_ballot_w64(cnt > 0);
+    const uint64_t m_full = __builtin_amdgcn_ballot_w64(cnt >= c);
+    auto col_ok = [&](int i) {
+        return __builtin_amdgcn_inverse_ballot_w64(i < cpart ? m_any : (i < c ? m_full : 0ull));
+    };
     constexpr int kRowsPerSet = kConeBlock / G;
     constexpr int rows_per_pass = NR * kRowsPerSet;
     constexpr int writer = G - 1;
@@ -2108,7 +2156,7 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
 #pragma unroll
                 for (int i = 0; i < CH; ++i) {
                     const float x = row[k][i];
-                    cp[k][i] = i < cnt ? x : 0.0f;
+                    cp[k][i] = (RT_SNR_SMASK ? col_ok(i) : i < cnt) ? x : 0.0f;
                     // the select on the float, before the fp64 conversion (else
                     // two selects on the converted halves)
                     asm("" : "+v"(cp[k][i]));
@@ -2213,7 +2261,7 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
 #pragma unroll
         for (int k = 0; k < NR; ++k)
 #pragma unroll
-            for (int i = 0; i < CH; ++i) cp[k][i] = i < cnt ? cp[k][i] : INFINITY;
+            for (int i = 0; i < CH; ++i) cp[k][i] = (RT_SNR_SMASK ? col_ok(i) : i < cnt) ? cp[k][i] : INFINITY;
         RT_SNR_MARK(7);
 #if RT_SNR_WAVE_LOCAL
         // a row's G <= 64 lanes are one wave, and a wave's LDS accesses
