@@ -218,9 +218,7 @@ def bench_cfg5(args, torch, dist, world, rank, local, dev):
         elapsed = time.perf_counter() - t0
         if world > 1:
             dist.barrier()
-            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed = float(t.item())
+            elapsed = rank_max(torch, dist, elapsed, dev)
         res[mode] = (elapsed, len(peaks))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -246,7 +244,7 @@ def bench_cfg5(args, torch, dist, world, rank, local, dev):
                                    "medium / long, smin 6), dispatch.search_files, DMIterator chunks of --batch "
                                    "files with the next chunk prefetched",
                        "files_per_gpu": files, "chunk": args.batch, "peaks_found": cold[1],
-                       "parallelism": f"dm-trials x{world} (independent, weak scaling)"},
+                       "parallelism": f"dm-trials x{world} (independent, weak scaling)" + REHEARSAL},
             "cold": {"value": total / cold[0], "seconds": cold[0]},
             "warm": {"value": total / warm[0], "seconds": warm[0], "peaks_found": warm[1]},
         }
@@ -257,6 +255,20 @@ def bench_cfg5(args, torch, dist, world, rank, local, dev):
 
 CFG3 = dict(n=1 << 22, tsamp=256e-6, pmin=0.2, pmax=5.0, bmin=240, bmax=260, ducy_max=0.2,
             rmed_width=4.0, rmed_minpts=101, trials=1024)
+
+
+# set by --one-gpu-rehearsal: every rank on cuda:0 over gloo (a code-path
+# check of the multi-rank legs, not a measurement)
+REHEARSAL = ""
+
+
+def rank_max(torch, dist, x, dev):
+    """Max of a float over the ranks (RCCL: a device tensor; gloo, the
+    one-GPU rehearsal: a host tensor)."""
+    on_dev = dist.get_backend() == "nccl"
+    t = torch.tensor([x], dtype=torch.float64, device=dev if on_dev else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def cfg3_trials(torch, ks, n, tsamp, device):
@@ -328,9 +340,7 @@ def bench_cfg3(args, torch, dist, world, rank, local, dev):
     plan.check()
     if world > 1:
         dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = rank_max(torch, dist, elapsed, dev)
     cone = engine.profile_read(0)
     stats = plan.stats()
     if rank == 0:
@@ -356,7 +366,7 @@ def bench_cfg3(args, torch, dist, world, rank, local, dev):
                 "trials_total": ntr, "trials_per_gpu": len(mine), "batch": B,
                 "trial_periods": plan.length, "ffa_transforms": stats["transforms"],
                 "cone_launches_per_batch": stats["launches"],
-                "parallelism": f"dm-trials x{world} (round-robin shard of one job, strong scaling)",
+                "parallelism": f"dm-trials x{world} (round-robin shard of one job, strong scaling)" + REHEARSAL,
             },
             "roofline": rf,
         }
@@ -378,6 +388,9 @@ def main():
     ap.add_argument("--files", type=int, default=256, help="cfg5: SIGPROC files per GPU")
     ap.add_argument("--trials", type=int, default=0, help="cfg3: trials in the job (default 1024)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--one-gpu-rehearsal", action="store_true",
+                    help="multi-rank code path check on a one-GPU box: every rank on cuda:0, gloo instead of "
+                         "RCCL (not a measurement)")
     ap.add_argument("--overlap", type=int, default=0, choices=(0, 1),
                     help="cfg2: 1 = step k+1's deredden + normalise + downsampling ladder on a second stream "
                          "while step k's FFA passes run (two workspaces); 0 = one stream")
@@ -397,10 +410,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.one_gpu_rehearsal:
+        global REHEARSAL
+        local = 0
+        REHEARSAL = " [one-GPU rehearsal: all ranks on cuda:0 over gloo, not a measurement]"
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.one_gpu_rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     if args.workload in ("cfg3", "cfg5"):
         (bench_cfg3 if args.workload == "cfg3" else bench_cfg5)(args, torch, dist, world, rank, local, dev)
         if world > 1:
@@ -457,9 +477,7 @@ def main():
     plan.check()                  # every timed step: no unit refused (the flag is sticky)
     if world > 1:
         dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = rank_max(torch, dist, elapsed, dev)
     cone = engine.profile_read(0)
     ladder = engine.profile_read(1)
     stats = plan.stats()
@@ -494,7 +512,7 @@ def main():
                 "scratch_mfloats_per_buffer_trial": float(os.environ["RIPTIDE_AMD_SCRATCH_MFLOATS"]),
                 "streams": "prep (deredden+normalise+ladder of step k+1) || FFA passes of step k" if args.overlap
                            else "one",
-                "parallelism": f"dm-trials x{world} (independent, weak scaling)",
+                "parallelism": f"dm-trials x{world} (independent, weak scaling)" + REHEARSAL,
             },
             "roofline": rf,
         }

@@ -418,6 +418,7 @@ rt_plan* make_plan(size_t size, double tsamp, const uint64_t* widths, size_t nw,
         P->ds_fused = !std::getenv("RIPTIDE_AMD_PER_RUNG_LADDER");
         for (const DsRung& d : P->rungs)
             if (!d.identity && std::ceil(d.f) + 2.0 > (double)kDsFusedMargin) P->ds_fused = false;
+        if (P->rungs.size() > kDsMaxRungs) P->ds_fused = false;
         ck(hipMalloc(&P->d_rungs, std::max<size_t>(1, P->rungs.size()) * sizeof(DsRung)), "hipMalloc");
         if (!P->rungs.empty())
             ck(hipMemcpy(P->d_rungs, P->rungs.data(), P->rungs.size() * sizeof(DsRung), hipMemcpyHostToDevice),

@@ -115,41 +115,69 @@ __device__ __forceinline__ uint64_t ds_first_output(double f, uint64_t s)
     return k;
 }
 
+// Outputs [k_lo, k_hi) of a rung whose window start floor(k f) lies in
+// [s0, s_end) (the block's span; s_end = n_in for the last block).
+__device__ __forceinline__ void ds_rung_range(const DsRung& r, uint64_t s0, uint64_t s_end, uint64_t n_in,
+                                              uint32_t& k_lo, uint32_t& k_hi)
+{
+    if (r.identity) {
+        k_lo = (uint32_t)min(s0, r.n);
+        k_hi = (uint32_t)min(s_end, r.n);
+        return;
+    }
+    k_lo = (uint32_t)min(ds_first_output(r.f, s0), r.n);
+    k_hi = (uint32_t)min(s_end >= n_in ? r.n : ds_first_output(r.f, s_end), r.n);
+}
+
+// Every rung's window sums over one staged span.  Indices are 32-bit (the
+// planner keeps every series below 2^29 samples), the start / end / floor
+// arithmetic is the reference's in float64 (downsample.hpp:53-75: (imin + 1)
+// - start is (floor(start) + 1.0) - start exactly, end - imax is end -
+// min(floor(end), N - 1)), and each rung's output range in the span is
+// computed once per block by one lane per rung instead of by every thread.
 __global__ __launch_bounds__(256) void downsample_fused_kernel(
     const float* __restrict__ x, uint64_t n_in, uint64_t x_stride,
     const DsRung* __restrict__ rungs, uint32_t num_rungs,
     float* __restrict__ out, uint64_t out_stride)
 {
     __shared__ float span[kDsSpanFloats];
+    __shared__ uint32_t kr[2 * kDsMaxRungs];
     const uint64_t s0 = (uint64_t)blockIdx.x * kDsFusedSpan;
     const uint64_t s_end = min(s0 + (uint64_t)kDsFusedSpan, n_in);     // window starts owned by this block
     const uint64_t l_end = min(s0 + (uint64_t)kDsSpanFloats, n_in);    // staged input
     x += (uint64_t)blockIdx.y * x_stride;
     out += (uint64_t)blockIdx.y * out_stride;
     for (uint64_t i = s0 + threadIdx.x; i < l_end; i += 256) span[i - s0] = x[i];
+    for (uint32_t ri = threadIdx.x; ri < num_rungs; ri += 256) {
+        uint32_t a, b;
+        ds_rung_range(rungs[ri], s0, s_end, n_in, a, b);
+        kr[2 * ri] = a;
+        kr[2 * ri + 1] = b;
+    }
     __syncthreads();
     const double last = (double)n_in - 1.0;
+    const uint32_t b0 = (uint32_t)s0;
     for (uint32_t ri = 0; ri < num_rungs; ++ri) {
         const DsRung r = rungs[ri];
         float* o = out + r.out_off;
+        const uint32_t k_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)kr[2 * ri]);
+        const uint32_t k_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)kr[2 * ri + 1]);
         if (r.identity) {
-            for (uint64_t k = s0 + threadIdx.x; k < min(s_end, r.n); k += 256) o[k] = span[k - s0];
+            for (uint32_t k = k_lo + threadIdx.x; k < k_hi; k += 256) o[k] = span[k - b0];
             continue;
         }
         const double f = r.f;
-        const uint64_t k_lo = ds_first_output(f, s0);
-        const uint64_t k_hi = min(s_end >= n_in ? r.n : ds_first_output(f, s_end), r.n);
-        for (uint64_t k = k_lo + threadIdx.x; k < k_hi; k += 256) {
+        for (uint32_t k = k_lo + threadIdx.x; k < k_hi; k += 256) {
             const double start = __dmul_rn((double)k, f);
             const double end = __dadd_rn(start, f);
-            const uint64_t imin = (uint64_t)floor(start);
+            const double fs = floor(start);
             double dmax = floor(end);
             if (dmax > last) dmax = last;
-            const uint64_t imax = (uint64_t)dmax;
-            const float wmin = (float)__dsub_rn((double)(imin + 1), start);
-            const float wmax = (float)__dsub_rn(end, (double)imax);
-            const float* w = span + (imin - s0);
-            const uint32_t cnt = (uint32_t)(imax - imin);
+            const uint32_t imin = (uint32_t)fs, imax = (uint32_t)dmax;
+            const float wmin = (float)__dsub_rn(__dadd_rn(fs, 1.0), start);
+            const float wmax = (float)__dsub_rn(end, dmax);
+            const float* w = span + (imin - b0);
+            const uint32_t cnt = imax - imin;
             o[k] = __fadd_rn(window_sum(w, wmin, cnt), __fmul_rn(wmax, w[cnt]));
         }
     }

@@ -259,6 +259,40 @@ def test_batch_matches_single(rt):
         assert np.array_equal(dn[b].cpu().numpy(), ref)
 
 
+def test_ladder_passes_pipeline_matches_run(rt):
+    """rt_periodogram_ladder_device + rt_periodogram_passes_device (the two
+    halves a pipelined caller runs on two streams, bench.py --overlap 1) give
+    exactly rt_periodogram_device's S/N: two batches with the second batch's
+    ladder on a side stream while the first batch's passes run, one
+    workspace per batch in flight."""
+    import torch
+    from riptide_amd import engine
+    case = inputs.PGRAM_CASES[1]
+    plan = engine.PeriodogramPlan.for_search(case["n"], case["tsamp"], case["pmin"], case["pmax"],
+                                             case["bmin"], case["bmax"], ducy_max=case["ducy_max"])
+    xs = [np.stack([inputs.with_signal(case["n"], case["tsamp"], s + 3 * k, 0.41, 12.0) for s in range(3)])
+          for k in range(2)]
+    ds = [torch.from_numpy(x).cuda() for x in xs]
+    ref = [plan.run(d).cpu().numpy() for d in ds]
+    ws = [torch.empty(plan.workspace_bytes(3), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    outs = [torch.empty((3, plan.length, plan.num_widths), dtype=torch.float32, device="cuda") for _ in range(2)]
+    main, side = torch.cuda.current_stream(), torch.cuda.Stream()
+    ev = [torch.cuda.Event() for _ in range(2)]
+    for k in range(2):
+        with torch.cuda.stream(side):
+            side.wait_stream(main)
+            plan.ladder(ds[k], ws[k], stream=side)
+            ev[k].record(side)
+        main.wait_event(ev[k])
+        plan.passes(outs[k], ws[k], stream=main)
+    torch.cuda.synchronize()
+    plan.check()
+    for k in range(2):
+        assert np.array_equal(outs[k].cpu().numpy(), ref[k])
+    with pytest.raises(ValueError):
+        plan.ladder(ds[0], torch.empty(16, dtype=torch.uint8, device="cuda"))
+
+
 @pytest.mark.parametrize("ducy_max, widths", [(0.2, None), (0.35, [1, 2, 5, 13, 40, 77, 91])])
 def test_wide_snr_matches_window_path(monkeypatch, ducy_max, widths):
     """Final units whose S/N reads the widths past its 12-column register
