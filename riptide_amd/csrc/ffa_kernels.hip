@@ -1241,6 +1241,19 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
     }
 }
 
+// final-pass rows zero-padded past p for unmasked S/N chunk reads (A/B knob):
+// 1 = zeros up to the row stride (same box, cone ms per cfg2 trial 7.98 /
+// 7.97 with it vs 7.86 / 7.81 without -- the merge's extra zero stores and
+// the second S/N read path cost more than the 17 column selects per row pass
+// they save); 2 = zeros only from the last slot's lanes past p, which store
+// anyway (no extra store), where every chunk up to the row's owner ends
+// inside the slots (cfg2 7.58 / 7.61 with it vs 7.53 / 7.48, cfg3 1.90 vs
+// 1.88: the 17 masking selects it removes sat in the shadow of the serial
+// fp64 prefix chain; profiles/r03z_ab_*.log)
+#ifndef RT_SNR_ZPAD
+#define RT_SNR_ZPAD 0
+#endif
+
 // Slot-step write-back into the dense LDS rows at base / store to global
 // memory (a non-final pass's output level): register rows 2q, 2q + 1 to the
 // slot's rows A and B.
@@ -1271,7 +1284,7 @@ __device__ __forceinline__ void write_rows_slots(float* base, float* dummy, cons
                     if (k < SMAX - 1) orow[64 * k] = v[i][k];
                     else *((tail_ok || tail_zero) ? orow + 64 * k : dummy) = tail_ok ? v[i][k] : 0.0f;
                 }
-                if (zpad && 64 * SMAX < q) *(rest_zero ? orow + 64 * SMAX : dummy) = 0.0f;
+                if (RT_SNR_ZPAD == 1 && zpad && 64 * SMAX < q) *(rest_zero ? orow + 64 * SMAX : dummy) = 0.0f;
             }
         }
     }
@@ -2089,6 +2102,13 @@ __device__ __forceinline__ float grp_allmax(float v)
 #ifndef RT_SNR_WAVE_LOCAL
 #define RT_SNR_WAVE_LOCAL 1
 #endif
+// S/N prefix values as offset + the first pass's running sums (snr_rows).
+// A/B knob, off: neutral (cone ms per cfg2 trial 7.689 / 7.700 with it vs
+// 7.688 / 7.700, profiles/r03za_ab_*.log), and the second serial pass keeps
+// the reference's association of the row's additions after each lane's offset
+#ifndef RT_SNR_RUNSUM
+#define RT_SNR_RUNSUM 0
+#endif
 // S/N column masks from two wave-uniform lane masks (snr_rows col_ok).  A/B
 // knob, off: 17 fewer v_cmp per row pass, but cone ms per trial cfg2 7.76 vs
 // 7.68, cfg3 1.92 vs 1.91 with it (the SALU mask selects feed every column's
@@ -2194,6 +2214,13 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
         // +0.0 and are never -0.0, so the additions are exact no-ops)
 #pragma unroll
         for (int k = 0; k < NR; ++k) part[k] = 0.0;
+#if RT_SNR_RUNSUM
+        // the lane's running sums kept from the first pass, so the prefix
+        // values are offset + run[i]: independent additions after the scan
+        // instead of a second serial chain of CH (the float64 sums of the
+        // row's floats are exact, as the lane-partial scan already assumes)
+        double run[NR][CH];
+#endif
 #pragma unroll
         for (int i = 0; i < CH; ++i)
 #pragma unroll
@@ -2203,6 +2230,9 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
 #else
                 part[k] = part[k] + (double)cp[k][i];
 #endif
+#if RT_SNR_RUNSUM
+                run[k][i] = part[k];
+#endif
             }
         double acc[NR];
 #pragma unroll
@@ -2211,6 +2241,14 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
             acc[k] = dpp_d<0x138>(incl);              // wave_shr:1 -- lane g takes lane g - 1
             if (g == 0) acc[k] = 0.0;
         }
+#if RT_SNR_RUNSUM
+#pragma unroll
+        for (int i = 0; i < CH; ++i)
+#pragma unroll
+            for (int k = 0; k < NR; ++k) cp[k][i] = (float)(acc[k] + run[k][i]);
+#pragma unroll
+        for (int k = 0; k < NR; ++k) acc[k] = acc[k] + run[k][CH - 1];
+#else
 #pragma unroll
         for (int i = 0; i < CH; ++i)
 #pragma unroll
@@ -2222,6 +2260,7 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
 #endif
                 cp[k][i] = (float)acc[k];
             }
+#endif
         float sum[NR];
 #pragma unroll
         for (int k = 0; k < NR; ++k) sum[k] = __shfl((float)acc[k], owner, G);
@@ -2616,13 +2655,6 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
 #ifndef RT_PRIO_HALF
 #define RT_PRIO_HALF 0
 #endif
-// final-pass rows zero-padded past p for unmasked S/N chunk reads (A/B knob,
-// off: same box, cone ms per cfg2 trial 7.98 / 7.97 with it vs 7.86 / 7.81
-// without -- the merge's extra zero stores and the second S/N read path cost
-// more than the 17 column selects per row pass they save)
-#ifndef RT_SNR_ZPAD
-#define RT_SNR_ZPAD 0
-#endif
 // WIDE: final units whose S/N takes the widths past its register window as
 // plain LDS windows (snr_wide_ok; a separate instantiation, so the plans
 // without such widths run code without it)
@@ -2766,8 +2798,19 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
             // the S/N's chunks read without column masks (zero-padded rows):
             // a final pass whose output level the row-slot write-back stores
             // at the S/N stride with room for every lane's whole chunk
-            const bool zpad = RT_SNR_ZPAD && !st && L > 0 && C.slots && (a.flags & kConeFuse2) &&
-                              SMAX <= 5 && SMAX != kPack2 && qout >= p + kSnrMaxChunk;
+            bool zpad = RT_SNR_ZPAD && !st && L > 0 && C.slots && (a.flags & kConeFuse2) &&
+                        SMAX <= 5 && SMAX != kPack2 && qout >= p + kSnrMaxChunk;
+            if (RT_SNR_ZPAD == 2) {
+                // zeros only from the last slot's lanes past p (stores they
+                // issue anyway): every lane up to the row's owner must read
+                // its whole chunk inside the slots, [p, 64 SMAX), and those
+                // bins must lie inside the row stride
+                int G = 8;
+                while (G < 64 && (((p + G - 1) / G) | 1) > kSnrMaxChunk) G <<= 1;
+                int c = (p + G - 1) / G;
+                if (c < kSnrMaxChunk) c |= 1;
+                zpad = zpad && ((p - 1) / c + 1) * c <= 64 * SMAX && qout >= 64 * SMAX;
+            }
             if (L > 0 && !(a.flags & kConeDiagNoMerge))
                 merge_levels<SMAX, RW>(C, buf, p, L, tid, st_regs, rs, o0, a.flags, buf + kLdsBufFloats + 4 + (tid & 63),
                                        qout, zpad);
