@@ -220,6 +220,9 @@ int rt_diag_stamps(uint64_t* out8, int reset);
 /* Diagnostic builds: per-unit timeline records (8 words each: hw id | xcc << 32,
  * start, setup done, fill landed, merge done, end, unit, shape), up to cap. */
 int rt_diag_timeline(uint64_t* out, uint64_t cap, uint64_t* count);
+/* Diagnostic builds: index of each cone launch's first timeline record (one
+ * entry per launch since the last rt_diag_stamps reset), up to cap. */
+int rt_diag_launches(uint64_t* out, uint64_t cap, uint64_t* count);
 
 /* Plan statistics: transforms, work items, passes, cone launches per trial. */
 int rt_plan_stats(const rt_plan* plan, uint64_t* transforms, uint64_t* items, uint64_t* launches,

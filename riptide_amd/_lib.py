@@ -64,6 +64,7 @@ _SIGNATURES = {
     "rt_profile_reset": (_c_i, []),
     "rt_diag_stamps": (_c_i, [_pu64, _c_i]),
     "rt_diag_timeline": (_c_i, [_pu64, ctypes.c_uint64, _pu64]),
+    "rt_diag_launches": (_c_i, [_pu64, ctypes.c_uint64, _pu64]),
     "rt_plan_stats": (_c_i, [_vp, _pu64, _pu64, _pu64, _pd, _pd, _pu64]),
     "rt_convert_samples_device": (_c_i, [_vp, _c_sz, _c_i, _vp, _vp]),
     "rt_segment_order_stats_device": (_c_i, [_vp, _c_sz, _c_sz, _c_sz, _c_sz, _c_sz, _c_sz, _vp, _c_sz, _vp, _vp]),

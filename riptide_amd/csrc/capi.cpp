@@ -225,6 +225,7 @@ struct DevicePlan {
 // Per-phase cycle counters of the cone kernel (RT_STAMPS diagnostic builds).
 unsigned long long* g_stamps = nullptr;
 uint64_t g_stamp_units = 0;      // unit records written since the last reset
+std::vector<uint64_t> g_stamp_launch;   // first record of each launch since the last reset
 
 // Run all cone launches of an exec plan.
 void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStream_t s)
@@ -245,6 +246,7 @@ void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStrea
             std::lock_guard<std::mutex> lk(g_prof.mu);
             if (g_stamp_units + units <= kTimelineCap) {
                 a.stamps = g_stamps + g_stamp_units * kStampRecWords;
+                g_stamp_launch.push_back(g_stamp_units);
                 g_stamp_units += units;
             }
         }
@@ -1194,8 +1196,23 @@ int rt_diag_stamps(uint64_t* out8, int reset)
         }
         ck(hipDeviceSynchronize(), "hipDeviceSynchronize");
         for (int i = 0; i < 8; ++i) out8[i] = 0;
+        std::lock_guard<std::mutex> lk(g_prof.mu);
         out8[0] = g_stamp_units;
-        if (reset) g_stamp_units = 0;
+        if (reset) {
+            g_stamp_units = 0;
+            g_stamp_launch.clear();
+        }
+        return RT_OK;
+    });
+}
+
+int rt_diag_launches(uint64_t* out, uint64_t cap, uint64_t* count)
+{
+    return guarded([&] {
+        std::lock_guard<std::mutex> lk(g_prof.mu);
+        const uint64_t n = std::min<uint64_t>(g_stamp_launch.size(), cap);
+        for (uint64_t i = 0; i < n; ++i) out[i] = g_stamp_launch[i];
+        *count = n;
         return RT_OK;
     });
 }

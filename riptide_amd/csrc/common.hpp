@@ -244,7 +244,7 @@ enum : uint8_t { kModeWhole = 0, kModeTile = 1 };
 // fill issued, descriptors built, fill landed, merge done, end), shape bits.
 constexpr int kStampMarks = 14;   // + S/N pass 0: prefix, barrier, window, end; + unit_begin: view, header, DMA issued
 constexpr int kStampRecWords = kStampMarks + 2;
-constexpr uint64_t kTimelineCap = 1u << 21;
+constexpr uint64_t kTimelineCap = 1u << 23;
 // cone kernel feature bits (ConeArgs::flags)
 enum : uint32_t {
     kConeStoreFromRegs = 1u,   // non-final passes store the output level straight from registers

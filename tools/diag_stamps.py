@@ -28,14 +28,13 @@ def main():
     import torch
     from riptide_amd import _lib, engine
     L = _lib.load()
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from bench_configs import CONFIGS
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-    cfg = sys.argv[2] if len(sys.argv) > 2 else "cfg2"
-    if cfg == "cfg4":
-        n = 1 << 22
-        plan = engine.PeriodogramPlan.for_search(n, 64e-6, 0.002, 0.5, 16, 32, ducy_max=0.2)
-    else:
-        n = 1 << 23
-        plan = engine.PeriodogramPlan.for_search(n, 256e-6, 0.1, 10.0, 240, 260, ducy_max=0.05)
+    c = {k["name"]: k for k in CONFIGS}[sys.argv[2] if len(sys.argv) > 2 else "cfg2"]
+    n = c["n"]
+    plan = engine.PeriodogramPlan.for_search(n, c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"],
+                                             ducy_max=c["ducy_max"])
     buf = (ctypes.c_uint64 * 8)()
     _lib.check(L.rt_diag_stamps(buf, 1))     # allocates the device records
     x = torch.randn((B, n), device="cuda", dtype=torch.float32)
@@ -44,14 +43,50 @@ def main():
     _lib.check(L.rt_diag_stamps(buf, 1))
     out = plan.run(x, out=out)
     torch.cuda.synchronize()
-    cap = 1 << 21
+    cap = 1 << 23
     rec = np.zeros(cap * REC, dtype=np.uint64)
     cnt = ctypes.c_uint64(0)
     _lib.check(L.rt_diag_timeline(rec.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), cap, ctypes.byref(cnt)))
     nrec = int(cnt.value)
     e = rec[:nrec * REC].reshape(nrec, REC).astype(np.int64)
-    e = e[e[:, 1] != 0]                      # units that returned early write nothing
-    print(json.dumps(analyse(e)))
+    starts = np.zeros(4096, dtype=np.uint64)
+    _lib.check(L.rt_diag_launches(starts.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), starts.size,
+                                  ctypes.byref(cnt)))
+    starts = starts[:int(cnt.value)].astype(np.int64)
+    keep = e[:, 1] != 0                      # units that returned early write nothing
+    launch = np.searchsorted(starts, np.nonzero(keep)[0], side="right") - 1
+    e = e[keep]
+    out = analyse(e)
+    out["config"], out["batch"] = c["name"], B
+    out["launch_tails"] = launch_tails(e, launch)
+    print(json.dumps(out))
+
+
+def launch_tails(e, launch, slots_per_xcd=64):
+    """Per cone launch and XCD (s_memtime counts are comparable within an
+    XCD): duration = last workgroup exit - first entry, tail = last exit -
+    median exit, idle = 1 - busy workgroup time / (slots x duration).
+    Sums over launches and XCDs, so the fractions weight long launches."""
+    xcc = (e[:, 0] >> 32) & 0xF
+    t_in, t_out = e[:, 1 + 5], e[:, 1 + 6]
+    dur = tail = busy = 0.0
+    per = []
+    for li in np.unique(launch):
+        ml = launch == li
+        d_l = t_l = 0.0
+        for x in np.unique(xcc[ml]):
+            m = ml & (xcc == x)
+            d = float(t_out[m].max() - t_in[m].min())
+            tl = float(t_out[m].max() - np.median(t_out[m]))
+            dur += d
+            tail += tl
+            busy += float((t_out[m] - t_in[m]).sum()) / slots_per_xcd
+            d_l, t_l = d_l + d, t_l + tl
+        per.append((int(ml.sum()), d_l, t_l))
+    per.sort(key=lambda r: -r[1])
+    return {"launches": len(per), "tail_frac": round(tail / dur, 4), "idle_slot_frac": round(1 - busy / dur, 4),
+            "longest": [{"units": u, "tail_frac": round(t / d, 4)} for u, d, t in per[:5]],
+            "shortest": [{"units": u, "tail_frac": round(t / d, 4)} for u, d, t in per[-3:]]}
 
 
 def analyse(e):
