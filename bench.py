@@ -399,10 +399,16 @@ def main():
         args.batch = 32 if args.workload == "cfg3" else 16
 
     # transform-group scratch per ping/pong buffer and trial (capi.cpp
-    # scratch_budget_floats): 384 M floats = 26 instead of 94 cone launches per
-    # step, ~1 % faster (tools/ab_sched.py); 49 GB of the 288 GB HBM at 16 trials
+    # scratch_budget_floats, tools/ab_sched.py): cfg2 at 1536 M floats puts
+    # the whole plan in one group, 14 cone launches per step instead of 51 at
+    # 384 M, 2.5 % faster (profiles/r03zd_sched_cfg2.jsonl), for 175 GB of
+    # workspace at 16 trials (53 GB at 384 M), so only where it fits: one
+    # workspace, one rank per GPU, and enough free HBM (checked below); cfg3
+    # at 32 trials has 14 launches at 384 M already
+    user_scratch = "RIPTIDE_AMD_SCRATCH_MFLOATS" in os.environ
     if args.workload in ("cfg2", "cfg3"):
-        os.environ.setdefault("RIPTIDE_AMD_SCRATCH_MFLOATS", "384")
+        big = args.workload == "cfg2" and not args.overlap and not args.one_gpu_rehearsal
+        os.environ.setdefault("RIPTIDE_AMD_SCRATCH_MFLOATS", "1536" if big else "384")
     import torch
     import torch.distributed as dist
     from riptide_amd import engine
@@ -431,6 +437,15 @@ def main():
     plan = engine.PeriodogramPlan.for_search(c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"],
                                              ducy_max=c["ducy_max"], device=local)
     B = args.batch
+    if not user_scratch and os.environ["RIPTIDE_AMD_SCRATCH_MFLOATS"] != "384":
+        # the one-group schedule only if its workspace + the step's buffers
+        # leave 10 % of the free HBM; else the 384 M groups
+        need = plan.workspace_bytes(B) + 4 * B * (plan.length * plan.num_widths + 3 * c["n"])
+        if need > 0.9 * torch.cuda.mem_get_info(dev)[0]:
+            os.environ["RIPTIDE_AMD_SCRATCH_MFLOATS"] = "384"
+            del plan
+            plan = engine.PeriodogramPlan.for_search(c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"],
+                                                     c["bmax"], ducy_max=c["ducy_max"], device=local)
     ws_samples = int(round(c["rmed_width"] / c["tsamp"]))
     raw = synth_batch(torch, B, c["n"], c["tsamp"], 1000 + rank, dev)
     xbuf = torch.empty_like(raw)

@@ -242,7 +242,8 @@ enum : uint8_t { kModeWhole = 0, kModeTile = 1 };
 // RT_STAMPS diagnostic builds: one record per work unit of kStampRecWords
 // words: hw id | xcc << 32, kStampMarks s_memtime marks (start, setup done,
 // fill issued, descriptors built, fill landed, merge done, end), shape bits.
-constexpr int kStampMarks = 14;   // + S/N pass 0: prefix, barrier, window, end; + unit_begin: view, header, DMA issued
+constexpr int kStampMarks = 16;   // + S/N pass 0: prefix, barrier, window, end; + unit_begin: view, header, DMA issued;
+                                   // + workgroup entry / exit on the device-wide 100 MHz clock
 constexpr int kStampRecWords = kStampMarks + 2;
 constexpr uint64_t kTimelineCap = 1u << 23;
 // cone kernel feature bits (ConeArgs::flags)

@@ -2701,6 +2701,7 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
 #endif
 #ifdef RT_STAMPS
     const unsigned long long t_entry = __builtin_amdgcn_s_memtime();
+    const unsigned long long r_entry = __builtin_amdgcn_s_memrealtime();
     unsigned long long t_begin[3] = {};
 #endif
     const uint32_t total = a.num_items * a.batch;
@@ -2843,6 +2844,8 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
         tl[13] = t_begin[2];
         if (kConeBuffers == 1 && (a.flags & kConeDiagExitWait)) __builtin_amdgcn_s_waitcnt(0x0F70);
         RT_MARK(6);
+        tl[14] = r_entry;
+        tl[15] = __builtin_amdgcn_s_memrealtime();
         if (tid == 0 && a.stamps) {
             unsigned long long* e = a.stamps + (uint64_t)kStampRecWords * (uint64_t)u;
             const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));     // HW_REG_HW_ID

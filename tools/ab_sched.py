@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
-"""Schedule A/B on the cfg2 workload: transform-group scratch budget
+"""Schedule A/B on one BASELINE config (default cfg2): transform-group scratch budget
 (RIPTIDE_AMD_SCRATCH_MFLOATS, read at plan creation) x number of HIP streams
 the batch is split over (each stream runs its share of the trials with its
 own workspace, so one stream's launch tails overlap the other's work).
 Prints ms per trial and whether the S/N equals the first configuration's.
 
-usage (GPU box): python tools/ab_sched.py 96:1,96:2,384:1 [batch]
+usage (GPU box): python tools/ab_sched.py 96:1,96:2,384:1 [batch] [cfg1|cfg2|cfg3|cfg4]
 """
 import json
 import os
@@ -19,14 +19,18 @@ sys.path.insert(0, REPO)
 def main():
     import torch
     from riptide_amd import engine
-    n = 1 << 23
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from bench_configs import CONFIGS
+    c = {k["name"]: k for k in CONFIGS}[sys.argv[3] if len(sys.argv) > 3 else "cfg2"]
+    n = c["n"]
     cfgs = [tuple(int(v) for v in c.split(":")) for c in (sys.argv[1] if len(sys.argv) > 1 else "96:1,96:2").split(",")]
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 16
     x = torch.randn((B, n), device="cuda", dtype=torch.float32)
     ref = None
     for scratch, ns in cfgs:
         os.environ["RIPTIDE_AMD_SCRATCH_MFLOATS"] = str(scratch)
-        plan = engine.PeriodogramPlan.for_search(n, 256e-6, 0.1, 10.0, 240, 260, ducy_max=0.05)
+        plan = engine.PeriodogramPlan.for_search(n, c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"],
+                                                 ducy_max=c["ducy_max"])
         out = torch.empty((B, plan.length, plan.num_widths), device="cuda", dtype=torch.float32)
         parts = [(k * B // ns, (k + 1) * B // ns) for k in range(ns)]
         streams = [torch.cuda.Stream() for _ in range(ns)]
@@ -54,7 +58,8 @@ def main():
             ref = out.clone()
         else:
             same = bool(torch.equal(ref, out))
-        print(json.dumps({"scratch_mfloats": scratch, "streams": ns, "batch": B, "launches": plan.stats()["launches"],
+        print(json.dumps({"config": c["name"], "scratch_mfloats": scratch,
+                          "workspace_gb": sum(w.numel() for w in wss) / 1e9, "streams": ns, "batch": B, "launches": plan.stats()["launches"],
                           "ms_per_trial": dt * 1e3, "identical_to_first": same}), flush=True)
         del out, wss, plan
         torch.cuda.empty_cache()

@@ -19,7 +19,7 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
-MARKS = 14
+MARKS = 16
 REC = MARKS + 2
 PHASES = ["wait", "begin_next", "merge", "tail"]
 
@@ -62,31 +62,31 @@ def main():
     print(json.dumps(out))
 
 
-def launch_tails(e, launch, slots_per_xcd=64):
-    """Per cone launch and XCD (s_memtime counts are comparable within an
-    XCD): duration = last workgroup exit - first entry, tail = last exit -
-    median exit, idle = 1 - busy workgroup time / (slots x duration).
-    Sums over launches and XCDs, so the fractions weight long launches."""
-    xcc = (e[:, 0] >> 32) & 0xF
-    t_in, t_out = e[:, 1 + 5], e[:, 1 + 6]
-    dur = tail = busy = 0.0
+def launch_tails(e, launch, slots=512):
+    """Per cone launch, on the device-wide 100 MHz clock (s_memrealtime at
+    workgroup entry and exit): duration = last exit - first entry, tail =
+    last exit - median exit, idle = 1 - busy workgroup time / (slots x
+    duration) with slots = 2 workgroups x 256 CUs, drain = last exit - last
+    entry (no unit left to start: the launch's tail proper).  Sums over
+    launches, so the fractions weight long launches; times in microseconds."""
+    t_in, t_out = e[:, 1 + 14], e[:, 1 + 15]
+    dur = tail = busy = drain = 0.0
     per = []
     for li in np.unique(launch):
-        ml = launch == li
-        d_l = t_l = 0.0
-        for x in np.unique(xcc[ml]):
-            m = ml & (xcc == x)
-            d = float(t_out[m].max() - t_in[m].min())
-            tl = float(t_out[m].max() - np.median(t_out[m]))
-            dur += d
-            tail += tl
-            busy += float((t_out[m] - t_in[m]).sum()) / slots_per_xcd
-            d_l, t_l = d_l + d, t_l + tl
-        per.append((int(ml.sum()), d_l, t_l))
+        m = launch == li
+        d = float(t_out[m].max() - t_in[m].min())
+        drain += float(t_out[m].max() - t_in[m].max())
+        tl = float(t_out[m].max() - np.median(t_out[m]))
+        dur += d
+        tail += tl
+        busy += float((t_out[m] - t_in[m]).sum()) / slots
+        per.append((int(m.sum()), d, tl))
     per.sort(key=lambda r: -r[1])
-    return {"launches": len(per), "tail_frac": round(tail / dur, 4), "idle_slot_frac": round(1 - busy / dur, 4),
-            "longest": [{"units": u, "tail_frac": round(t / d, 4)} for u, d, t in per[:5]],
-            "shortest": [{"units": u, "tail_frac": round(t / d, 4)} for u, d, t in per[-3:]]}
+    us = 0.01
+    return {"launches": len(per), "sum_duration_us": round(dur * us, 1), "tail_frac": round(tail / dur, 4),
+            "drain_frac": round(drain / dur, 4), "idle_slot_frac": round(1 - busy / dur, 4),
+            "longest": [{"units": u, "us": round(d * us, 1), "tail_us": round(t * us, 1)} for u, d, t in per[:5]],
+            "shortest": [{"units": u, "us": round(d * us, 1), "tail_us": round(t * us, 1)} for u, d, t in per[-3:]]}
 
 
 def analyse(e):
