@@ -1804,7 +1804,7 @@ __device__ __forceinline__ double dpp_d_rows(double v)
     return __hiloint2double(hi, lo);
 }
 
-// Inclusive scan over each G-lane group (G = 8 .. 64): row_shr steps inside
+// Inclusive scan over each G-lane group (G = 2 .. 64): row_shr steps inside
 // 16-lane rows, then row_bcast:15 / row_bcast:31 across rows.  The partial
 // sums start at +0.0 and are never -0.0, so adding the +0.0 that masked
 // lanes receive is an exact no-op.
@@ -1814,10 +1814,14 @@ __device__ __forceinline__ double seg_scan_dpp(double v, int lane)
     const int g = lane & (G < 16 ? G - 1 : 15);     // position inside the group's part of the 16-lane row
     double y = dpp_d<0x111>(v);
     v = g >= 1 ? v + y : v;
-    y = dpp_d<0x112>(v);
-    v = g >= 2 ? v + y : v;
-    y = dpp_d<0x114>(v);
-    v = g >= 4 ? v + y : v;
+    if (G >= 4) {
+        y = dpp_d<0x112>(v);
+        v = g >= 2 ? v + y : v;
+    }
+    if (G >= 8) {
+        y = dpp_d<0x114>(v);
+        v = g >= 4 ? v + y : v;
+    }
     if (G >= 16) {
         y = dpp_d<0x118>(v);
         v = g >= 8 ? v + y : v;
@@ -1854,7 +1858,7 @@ __device__ __forceinline__ float seg_max_dpp(float v, int lane)
         if (G >= 32) v = fmaxf(v, dpp_keep_rows<0x142, 0xA>(v));
         if (G >= 64) v = fmaxf(v, dpp_keep_rows<0x143, 0xC>(v));
     } else {
-        const int g = lane & 7;
+        const int g = lane & (G - 1);
         float y = dpp_keep<0x111>(v);
         v = g >= 1 ? fmaxf(v, y) : v;
         y = dpp_keep<0x112>(v);
@@ -2070,21 +2074,22 @@ __device__ __forceinline__ void snr_width_consts(int w, int p, float* out)
 #endif
 constexpr bool kSnrTransEmit = RT_SNR_TEMIT != 0;
 
-// max over each G-lane group (G = 8 .. 64, groups aligned), in every lane
+// max over each G-lane group (G = 2 .. 64, groups aligned), in every lane
 // of the group: quad swaps, then the half-row and row mirrors, then (G >= 32)
 // cross-row exchanges (max never returns a NaN operand over a number, as
 // diff_max's comparison)
 template <int G>
 __device__ __forceinline__ float grp_allmax(float v)
 {
-    static_assert(G == 8 || G == 16 || G == 32 || G == 64, "lane groups");
+    static_assert(G == 2 || G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "lane groups");
     // v_max_f32 with a DPP source (no canonicalising moves around a
     // separate DPP move); s_nop 1: the DPP read of a VGPR written by the
     // previous VALU instruction
-    asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-                 "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
-                 "s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf"
-                 : "+v"(v));
+    asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(v));
+    if constexpr (G >= 4)
+        asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf" : "+v"(v));
+    if constexpr (G >= 8)
+        asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf" : "+v"(v));
     if constexpr (G >= 16)
         asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf" : "+v"(v));
     // 32- and 64-lane groups: lane i <-> i ^ 16 by ds_swizzle (xor mask 16
@@ -2531,6 +2536,16 @@ constexpr bool variant_has_group(int smax, int G)
     return snr_group(variant_pmin(smax)) <= G && G <= snr_group(variant_pmax(smax));
 }
 
+// S/N lane-group size of the short-row variant (kPack2, p <= 32): 2, 4 or 8
+// lanes per row (8 = the general rule, snr_group).  A/B, same box, cone ms
+// per cfg4 trial (profiles/r03zf_ab_cfg4.log): G = 8 0.837 / 0.837, G = 4
+// 0.777 / 0.778, G = 2 0.796 / 0.797, S/N identical -- 4.
+#ifndef RT_SNR_SHORT_G
+#define RT_SNR_SHORT_G 4
+#endif
+constexpr int kSnrShortG = RT_SNR_SHORT_G;
+static_assert(kSnrShortG == 2 || kSnrShortG == 4 || kSnrShortG == 8, "RT_SNR_SHORT_G is 2, 4 or 8");
+
 template <int SMAX, bool WIDE = false>
 __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& U, float* data, int q, const int* wl,
                                              int nrows, int tid, float* whb, unsigned long long* tl, bool zpad = false)
@@ -2553,6 +2568,17 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
     if (c < kSnrMaxChunk) c |= 1;
     const uint32_t nw = a.num_widths;
     float* snr = a.snr + (uint64_t)U.trial * a.snr_stride + (U.snr_row + (uint64_t)U.s0) * (uint64_t)nw;
+    if constexpr (SMAX == kPack2 && kSnrShortG < 8) {
+        // short rows (p <= 32): kSnrShortG lanes per row, so a pass covers
+        // 512 / G rows (cfg4's ~380-row final units: 3 passes at G = 4
+        // instead of 6 at G = 8)
+        constexpr int GS = kSnrShortG;
+        const int cs = ((p + GS - 1) / GS) | 1;
+        if (cs <= 5) snr_rows<5, GS>(a, U, data, q, wl, nev, cs, tid, whb, tl, zpad);
+        else if (cs <= 9) snr_rows<9, GS>(a, U, data, q, wl, nev, cs, tid, whb, tl, zpad);
+        else snr_rows<kSnrMaxChunk, GS>(a, U, data, q, wl, nev, cs, tid, whb, tl, zpad);
+        return;
+    }
     if (c <= kSnrMaxChunk) {
         // short rows (p <= 40 / 72): register chunks sized to the row, not 17
         if constexpr (variant_has_group(SMAX, 8)) {
