@@ -228,6 +228,25 @@ hipError_t launch_downsample_ladder(const float* x, uint64_t n_in, uint64_t x_st
 // Whole units compute their descriptors on the fly (node partition
 // arithmetic, no table).
 
+// Cache policy bits (gfx950: 1 sc0, 2 nt, 16 sc1) of the fill's LDS-DMA
+// loads, of the merge passes' output stores and of the S/N stores.  A/B,
+// same box, cone ms per trial (profiles/r03zg_ab_*.log): nt stores cfg2
+// 7.663 -> 7.616, cfg3 1.907 -> 1.883 (the next pass reads them from HBM
+// anyway); nt fills 7.86 / 1.94, slower (adjacent tiles' cones overlap and
+// share their L2 lines) -- stores nt, fills default.  Only the whole-slot
+// stores (64 consecutive words per wave instruction) are nt: the short-row
+// stores (4-byte scattered per lane) took cfg4 from 0.776 to 1.306 ms per
+// trial with nt (r03zh_ab_cfg4.log) and keep the default.
+#ifndef RT_FILL_CPOL
+#define RT_FILL_CPOL 0
+#endif
+#ifndef RT_STORE_CPOL
+#define RT_STORE_CPOL 2
+#endif
+#ifndef RT_SNR_CPOL
+#define RT_SNR_CPOL 0
+#endif
+
 // LDS-only workgroup barrier: orders LDS accesses without waiting for the
 // global loads or stores that are still in flight.
 __device__ __forceinline__ void lds_barrier()
@@ -356,7 +375,7 @@ __device__ __forceinline__ void dma_run(__amdgpu_buffer_rsrc_t rs, uint32_t goff
         const int c = c0 + lane;
         if (c < nch)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds + 4 * c0), 16,
-                                                     (int)(goff + 16u * (uint32_t)c), 0, 0, 0);
+                                                     (int)(goff + 16u * (uint32_t)c), 0, 0, RT_FILL_CPOL);
     }
 }
 
@@ -448,7 +467,7 @@ __device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t u, uin
                 const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)sv.z, i);
                 if (lane < n && 4 * (c0 + n) <= kLdsBufFloats && !(a.flags & kConeDiagNoFill))
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(buf + 4 * c0),
-                                                             16, (int)((g + (uint32_t)lane) * 16u), 0, 0, 0);
+                                                             16, (int)((g + (uint32_t)lane) * 16u), 0, 0, RT_FILL_CPOL);
             }
         }
     }
@@ -718,10 +737,10 @@ __device__ __forceinline__ void store_rows(const float (&v)[RW][SMAX], int p, in
                     // store out of the buffer's range, which drops them
                     const uint32_t o = k < SMAX - 1 ? ob + 256u * (uint32_t)k
                                                     : (tail_ok ? ob + 256u * (uint32_t)k : 0x80000000u);
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs, (int)o, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs, (int)o, 0, RT_STORE_CPOL);
                 } else if (64 * (k + 1) <= p || (k < S && lane + 64 * k < p)) {
                     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs,
-                                                          (int)(ob + 256u * (uint32_t)k), 0, 0);
+                                                          (int)(ob + 256u * (uint32_t)k), 0, RT_STORE_CPOL);
                 }
             }
         }
@@ -1309,7 +1328,7 @@ __device__ __forceinline__ void store_rows_slots(const float (&v)[RW][SMAX], int
                 for (int k = 0; k < SMAX; ++k) {
                     const uint32_t o = k < SMAX - 1 ? ob + 256u * (uint32_t)k
                                                     : (tail_ok ? ob + 256u * (uint32_t)k : 0x80000000u);
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs, (int)o, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs, (int)o, 0, RT_STORE_CPOL);
                 }
             }
         }
@@ -2379,7 +2398,7 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
                 for (int k = 0; k < NR; ++k) {
                     const float dm = seg_max_dpp<G>(dmax[k], lane);
                     const float v = (hpb * dm - b * sum[k]) / U.stdnoise;
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srs, (int)(so[k] + iw * 4u), 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srs, (int)(so[k] + iw * 4u), 0, RT_SNR_CPOL);
                 }
             }
         };
@@ -2517,7 +2536,7 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
                         const float v = (hpb * sel[k][sl] - b * sum[k]) / U.stdnoise;
                         const uint32_t o = (active[k] && iw < (int)nw) ? ((uint32_t)r[k] * nw + (uint32_t)iw) * 4u
                                                                        : 0x80000000u;
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srs, (int)o, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srs, (int)o, 0, RT_SNR_CPOL);
                     }
                 }
             }
@@ -2851,7 +2870,7 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
                     for (int r = 0; r < n0; ++r)
                         for (int j = tid; j < p; j += kConeBlock)
                             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(obase[r * qst + j]), rs,
-                                                                  (int)(o0 + (uint32_t)(r * p + j) * 4u), 0, 0);
+                                                                  (int)(o0 + (uint32_t)(r * p + j) * 4u), 0, RT_STORE_CPOL);
                 }
             } else {
 #ifdef RT_STAMPS
