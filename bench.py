@@ -59,16 +59,18 @@ def source_digest():
     return h.hexdigest()[:16]
 
 
-def pmc_traffic():
+def pmc_traffic(workload="cfg2"):
     """HBM bytes per trial of the cone kernel from the newest committed PMC
-    summary (profiles/*_pmc_cone.json, written by tools/pmc_to_json.py from
-    rocprofv3 FETCH_SIZE/WRITE_SIZE passes).  Returns (summary or None,
-    reason): a summary measured on other kernel sources than these
-    (`csrc_sha` != source_digest()) is stale and not used."""
+    summary of this workload (profiles/*_pmc_cone.json for cfg2,
+    profiles/*_pmc_cone_<cfg>.json for the others; written by
+    tools/pmc_to_json.py from rocprofv3 FETCH_SIZE/WRITE_SIZE passes).
+    Returns (summary or None, reason): a summary measured on other kernel
+    sources than these (`csrc_sha` != source_digest()) is stale and not used."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_cone.json")))   # r01a < r01b < ...: newest last
+    pat = "*_pmc_cone.json" if workload == "cfg2" else f"*_pmc_cone_{workload}.json"
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", pat)))   # r01a < r01b < ...: newest last
     if not files:
-        return None, "no PMC summary under profiles/"
+        return None, f"no {workload} PMC summary under profiles/"
     with open(files[-1]) as f:
         d = json.load(f)
     src = os.path.relpath(files[-1], REPO)
@@ -176,6 +178,12 @@ def bench_cfg5(args, torch, dist, world, rank, local, dev):
     # ~8 MiB (8-bit) / 32 MiB (float32) per file; leave 20 % of the disk free
     free = shutil.disk_usage(root).free
     files = max(2 * args.batch, min(files, int(0.8 * free / world / (34 << 20))))
+    if world > 1:
+        # every rank must agree on the node's file list before any writes:
+        # the smallest count over ranks (each measured the disk before writing)
+        t = torch.tensor([files], dtype=torch.int64, device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        files = int(t.item())
     tmp = tempfile.mkdtemp(prefix=f"cfg5_r{rank}_", dir=root)
     # the node's file list (rank r writes the files it will search, k = r, r + world, ...)
     total = world * files
@@ -271,6 +279,33 @@ def rank_max(torch, dist, x, dev):
     return float(t.item())
 
 
+def self_check(torch, dist, engine, plan, xbuf, snr, c, local, world, dev):
+    """After the timed region: trial 0 of the last timed batch (its
+    dereddened + normalised series is still in xbuf[0]) through a plan with
+    the library's default transform grouping (96 Mi floats per buffer: the
+    schedule every GPU parity test runs); True on every rank only if its S/N
+    is bit-identical to the benchmarked schedule's (snr[0])."""
+    saved = os.environ.get("RIPTIDE_AMD_SCRATCH_MFLOATS")
+    os.environ.pop("RIPTIDE_AMD_SCRATCH_MFLOATS", None)
+    try:
+        ref = engine.PeriodogramPlan.for_search(c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"],
+                                                ducy_max=c["ducy_max"], device=local)
+    finally:
+        if saved is not None:
+            os.environ["RIPTIDE_AMD_SCRATCH_MFLOATS"] = saved
+    got = ref.run(xbuf[0:1].contiguous(), check=True)
+    torch.cuda.synchronize()
+    same = bool(torch.equal(got[0], snr[0]))
+    if not same:
+        bad = int((got[0] != snr[0]).sum().item())
+        print(f"bench self-check: {bad} S/N values of trial 0 differ from the default-schedule plan",
+              file=sys.stderr, flush=True)
+    del ref, got
+    if world > 1:
+        same = rank_max(torch, dist, 0.0 if same else 1.0, dev) == 0.0
+    return same
+
+
 def cfg3_trials(torch, ks, n, tsamp, device):
     """BASELINE configs[2] trials, generated on the device: trial k is white
     noise from a generator seeded k, plus a slow red-noise ramp; every 64th
@@ -344,7 +379,8 @@ def bench_cfg3(args, torch, dist, world, rank, local, dev):
     cone = engine.profile_read(0)
     stats = plan.stats()
     if rank == 0:
-        rf = roofline(engine, cone, stats, B)
+        pmc, pmc_reason = pmc_traffic("cfg3")
+        rf = roofline(engine, cone, stats, B, pmc, pmc_reason)
         rf["kernel_ms_per_trial"] = cone["ms"] / (args.steps * len(mine))
         line = {
             "metric": "DM trials/sec (node), 1024-trial job at 2^22 samples, P=0.2-5 s (BASELINE configs[2])",
@@ -496,6 +532,7 @@ def main():
     cone = engine.profile_read(0)
     ladder = engine.profile_read(1)
     stats = plan.stats()
+    checked = self_check(torch, dist, engine, plan, xbuf, snr, c, local, world, dev)
 
     if rank == 0:
         pmc, pmc_reason = pmc_traffic()
@@ -530,6 +567,7 @@ def main():
                 "parallelism": f"dm-trials x{world} (independent, weak scaling)" + REHEARSAL,
             },
             "roofline": rf,
+            "checked": checked,
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baselines("cfg2")

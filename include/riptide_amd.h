@@ -112,6 +112,15 @@ int rt_schedule_check(size_t size, double tsamp, size_t num_widths, double perio
                       uint64_t* launches, double* alg_bytes_per_trial, double* moved_bytes_per_trial,
                       uint64_t* cells_per_trial);
 
+/* Host-only: the downsampling-ladder kernel a periodogram plan of these
+ * parameters runs (periodogram.hpp:162-168 restated per rung): *fused = 1
+ * for the one-read fused ladder (32-bit sample indices: series below 2^29
+ * samples, every rung's window inside its staging margin), 0 for the
+ * per-rung kernel (64-bit indices); *rungs = rungs that feed a transform.
+ * Either pointer may be NULL. */
+int rt_ladder_check(size_t size, double tsamp, double period_min, double period_max, size_t bins_min,
+                    size_t bins_max, int* fused, uint64_t* rungs);
+
 /* The pass schedule rt_ffa2 runs for one rows x cols transform, built and
  * validated on the host only (validate_exec_plan: tiles, LDS budgets, unit
  * blobs, DMA segments, row slots); no device needed.  *launches may be NULL. */
@@ -182,7 +191,7 @@ int rt_deredden_normalise_device(const float* d_in, size_t size, size_t batch, s
  * Order statistics of every (trial, width, segment): segment k covers rows
  * [k * per_seg, (k + 1) * per_seg) (segment_stats, peak_detection.py:71-82);
  * d_out[((b * W + iw) * nseg + k) * nranks + r] = the ranks[r]-th smallest S/N
- * of the segment (NaN if the segment holds a NaN).  per_seg <= 4096. */
+ * of the segment (NaN if the segment holds a NaN).  per_seg <= 32768. */
 int rt_segment_order_stats_device(const float* d_snrs, size_t batch, size_t snr_stride, size_t length,
                                   size_t num_widths, size_t nseg, size_t per_seg, const uint32_t* ranks,
                                   size_t nranks, float* d_out, void* stream);
@@ -228,12 +237,6 @@ int rt_diag_launches(uint64_t* out, uint64_t cap, uint64_t* count);
 int rt_plan_stats(const rt_plan* plan, uint64_t* transforms, uint64_t* items, uint64_t* launches,
                   double* alg_bytes_per_trial, double* moved_bytes_per_trial, uint64_t* cells_per_trial);
 
-/* TEST ONLY (no reference counterpart): while `on` is non-zero, every plan
- * uploaded to a device carries one unit that breaks the cone kernel's budget,
- * so the kernel refuses it and raises the plan's error flag -- exercises
- * rt_plan_check and the host-buffer API's error path.  The product never sets
- * it; tests/test_gpu_e2e.py::test_plan_device_error_flag does. */
-int rt_test_corrupt_next_plans(int on);
 
 #ifdef __cplusplus
 }

@@ -70,10 +70,17 @@ _SIGNATURES = {
     "rt_segment_order_stats_device": (_c_i, [_vp, _c_sz, _c_sz, _c_sz, _c_sz, _c_sz, _c_sz, _vp, _c_sz, _vp, _vp]),
     "rt_threshold_select_device": (_c_i, [_vp, _c_sz, _c_sz, _c_sz, _c_sz, _vp, _vp, _c_sz, _c_d, _vp, _vp, _c_sz,
                                           _vp]),
-    "rt_test_corrupt_next_plans": (_c_i, [_c_i]),   # test-only hook (tests/test_gpu_e2e.py)
+    "rt_ladder_check": (_c_i, [_c_sz, _c_d, _c_d, _c_d, _c_sz, _c_sz, ctypes.POINTER(_c_i), _pu64]),
 }
 
 EXPORTED = tuple(_SIGNATURES)
+
+# test build only (libriptide_amd_testhooks.so, include/riptide_amd_test.h);
+# bound when the loaded library has them
+_TEST_SIGNATURES = {
+    "rt_test_corrupt_next_plans": (_c_i, [_c_i]),
+}
+TESTHOOKS_PATH = os.path.join(_HERE, "libriptide_amd_testhooks.so")
 
 _lib = None
 
@@ -97,6 +104,11 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    for name, (res, args) in _TEST_SIGNATURES.items():
+        if hasattr(lib, name):
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
     _lib = lib
     return lib
 

@@ -1,6 +1,9 @@
 // C ABI of the engine (include/riptide_amd.h): host-buffer drop-ins for
 // riptide.libcpp and the device-resident batched periodogram.
 #include "riptide_amd.h"
+#ifdef RT_TEST_HOOKS
+#include "riptide_amd_test.h"
+#endif
 
 #include <hip/hip_runtime.h>
 
@@ -152,9 +155,11 @@ struct Profiler {
     }
 } g_prof;
 
-// test-only: plans uploaded while set carry one corrupt unit (never set by
-// the product; tests toggle it through rt_test_corrupt_next_plans)
+#ifdef RT_TEST_HOOKS
+// test builds only (libriptide_amd_testhooks.so): plans uploaded while set
+// carry one corrupt unit (tests toggle it through rt_test_corrupt_next_plans)
 std::atomic<int> g_test_corrupt{0};
+#endif
 
 // ---- a compiled plan resident on one device
 struct DevicePlan {
@@ -202,6 +207,7 @@ struct DevicePlan {
             }
             u[i] = d;
         }
+#ifdef RT_TEST_HOOKS
         // test-only hook (rt_test_corrupt_next_plans): give the first
         // whole-node unit more merge levels than any kernel instance runs,
         // after the host validation, so the kernel's own check refuses it and
@@ -212,6 +218,7 @@ struct DevicePlan {
                     d.levels = kMaxLevels + 1;
                     break;
                 }
+#endif
         ck(hipMalloc(&d_blob, std::max<size_t>(4, ex.blob.size()) * sizeof(uint32_t)), "hipMalloc");
         if (!ex.blob.empty())
             ck(hipMemcpy(d_blob, ex.blob.data(), ex.blob.size() * sizeof(uint32_t), hipMemcpyHostToDevice),
@@ -358,6 +365,45 @@ struct rt_plan {
 
 namespace {
 
+// The fused ladder (downsample_fused_kernel) indexes samples and outputs in
+// 32 bits and stages kDsFusedMargin floats past each span: series of 2^29
+// samples or more, rungs whose window (ceil(f) + 2) exceeds the margin, and
+// more rungs than its per-block table take the per-rung kernel (64-bit
+// indices) instead.
+constexpr uint64_t kDsFusedMaxSize = 1ull << 29;
+bool ladder_fusable(size_t size, const std::vector<DsRung>& rungs)
+{
+    if ((uint64_t)size >= kDsFusedMaxSize || rungs.size() > kDsMaxRungs) return false;
+    for (const DsRung& d : rungs)
+        if (!d.identity && std::ceil(d.f) + 2.0 > (double)kDsFusedMargin) return false;
+    return true;
+}
+
+// The rungs of a periodogram that feed at least one transform, in the
+// ladder kernels' form.
+std::vector<DsRung> used_rungs(const PgramPlan& pg)
+{
+    std::vector<bool> used(pg.rungs.size(), false);
+    for (const Step& s : pg.steps)
+        if (s.rows_eval) used[s.rung] = true;
+    std::vector<DsRung> out;
+    uint32_t blocks = 0;
+    for (size_t r = 0; r < pg.rungs.size(); ++r) {
+        if (!used[r]) continue;
+        const Rung& R = pg.rungs[r];
+        DsRung d{};
+        d.f = R.f;
+        d.n = R.n;
+        d.out_off = R.leaf_off;
+        d.first_block = blocks;
+        d.identity = R.f == 1.0;
+        ds_configure(d);
+        blocks += (uint32_t)((R.n + d.per_block - 1) / d.per_block);
+        out.push_back(d);
+    }
+    return out;
+}
+
 rt_plan* make_plan(size_t size, double tsamp, const uint64_t* widths, size_t nw, double pmin, double pmax,
                    size_t bmin, size_t bmax)
 {
@@ -400,27 +446,10 @@ rt_plan* make_plan(size_t size, double tsamp, const uint64_t* widths, size_t nw,
         ck(hipMalloc(&P->d_flag, sizeof(int)), "hipMalloc");
         ck(hipMemset(P->d_flag, 0, sizeof(int)), "hipMemset");
         // downsample ladder over the rungs that feed at least one transform
-        std::vector<bool> used(P->pg.rungs.size(), false);
-        for (const FfaXform& X : xf) used[X.rung] = true;
-        uint32_t blocks = 0;
-        for (size_t r = 0; r < P->pg.rungs.size(); ++r) {
-            if (!used[r]) continue;
-            const Rung& R = P->pg.rungs[r];
-            DsRung d{};
-            d.f = R.f;
-            d.n = R.n;
-            d.out_off = R.leaf_off;
-            d.first_block = blocks;
-            d.identity = R.f == 1.0;
-            ds_configure(d);
-            blocks += (uint32_t)((R.n + d.per_block - 1) / d.per_block);
-            P->rungs.push_back(d);
-        }
-        P->ds_blocks = blocks;
-        P->ds_fused = !std::getenv("RIPTIDE_AMD_PER_RUNG_LADDER");
-        for (const DsRung& d : P->rungs)
-            if (!d.identity && std::ceil(d.f) + 2.0 > (double)kDsFusedMargin) P->ds_fused = false;
-        if (P->rungs.size() > kDsMaxRungs) P->ds_fused = false;
+        P->rungs = used_rungs(P->pg);
+        P->ds_blocks = 0;
+        for (const DsRung& d : P->rungs) P->ds_blocks += (uint32_t)((d.n + d.per_block - 1) / d.per_block);
+        P->ds_fused = !std::getenv("RIPTIDE_AMD_PER_RUNG_LADDER") && ladder_fusable(prm.size, P->rungs);
         ck(hipMalloc(&P->d_rungs, std::max<size_t>(1, P->rungs.size()) * sizeof(DsRung)), "hipMalloc");
         if (!P->rungs.empty())
             ck(hipMemcpy(P->d_rungs, P->rungs.data(), P->rungs.size() * sizeof(DsRung), hipMemcpyHostToDevice),
@@ -948,6 +977,28 @@ int rt_ffa_schedule_check(size_t rows, size_t cols, uint64_t* launches)
     });
 }
 
+int rt_ladder_check(size_t size, double tsamp, double pmin, double pmax, size_t bmin, size_t bmax, int* fused,
+                    uint64_t* rungs)
+{
+    return guarded([&] {
+        PgramParams prm;
+        prm.size = size;
+        prm.tsamp = tsamp;
+        prm.pmin = pmin;
+        prm.pmax = pmax;
+        prm.bmin = bmin;
+        prm.bmax = bmax;
+        const std::string msg = check_pgram_args(prm);
+        if (!msg.empty()) throw std::invalid_argument(msg);
+        PgramPlan pg;
+        build_pgram_plan(prm, pg);
+        const std::vector<DsRung> r = used_rungs(pg);
+        if (fused) *fused = ladder_fusable(size, r) ? 1 : 0;
+        if (rungs) *rungs = r.size();
+        return RT_OK;
+    });
+}
+
 int rt_schedule_check(size_t size, double tsamp, size_t nw, double pmin, double pmax, size_t bmin, size_t bmax,
                       uint64_t* transforms, uint64_t* items, uint64_t* launches, double* alg_bytes,
                       double* moved_bytes, uint64_t* cells)
@@ -1252,8 +1303,10 @@ int rt_plan_stats(const rt_plan* P, uint64_t* transforms, uint64_t* items, uint6
 
 }  // extern "C"
 
+#ifdef RT_TEST_HOOKS
 int rt_test_corrupt_next_plans(int on)
 {
     g_test_corrupt.store(on ? 1 : 0, std::memory_order_relaxed);
     return RT_OK;
 }
+#endif

@@ -27,37 +27,25 @@
 
 namespace rt {
 
-// ---- cone kernel geometry (gfx950: 160 KiB LDS per CU).  Two layouts
-// (RT_CONE_BUFFERS):
-//   2: one persistent 1024-thread workgroup per CU (16 waves, <= 128 VGPRs)
-//      with two 70 KiB level buffers: it merges one unit in one buffer while
-//      the next unit's bottom level streams into the other by LDS DMA;
-//   1: two 512-thread workgroups per CU (8 waves each, <= 128 VGPRs), one
-//      71 KiB level buffer each: a unit's DMA is waited for at its start and
-//      the CU's other workgroup fills that wait.
-// The merged levels are dense rows (stride p).
-#ifndef RT_CONE_BUFFERS
-#define RT_CONE_BUFFERS 1
+// ---- cone kernel geometry (gfx950: 160 KiB LDS per CU): two 512-thread
+// workgroups per CU (8 waves each, <= 128 VGPRs), one 71 KiB level buffer
+// each; the CU's other workgroup fills one's fill and startup latency.  (The
+// one-16-wave-workgroup double-buffered layout and the 3- / 4-workgroup
+// layouts were measured slower: DESIGN.md section 5.)  The merged levels are
+// dense rows (stride p).
+constexpr int kConeWgsPerCu = 2;
+#ifndef RT_CONE_WAVES
+#define RT_CONE_WAVES 8
 #endif
-constexpr int kConeBuffers = RT_CONE_BUFFERS;
-static_assert(kConeBuffers == 1 || kConeBuffers == 2, "RT_CONE_BUFFERS is 1 or 2");
-// one buffer: workgroups per CU (2: 512 threads and a 71 KiB buffer each;
-// 4: 256 threads and a 35 KiB buffer each -- smaller units, more of them in
-// flight per CU)
-#ifndef RT_CONE_WGS
-#define RT_CONE_WGS 2
-#endif
-static_assert(RT_CONE_WGS >= 2 && RT_CONE_WGS <= 4, "RT_CONE_WGS is 2, 3 or 4");
-constexpr int kConeWgsPerCu = kConeBuffers == 2 ? 1 : RT_CONE_WGS;
-constexpr int kConeBlock = kConeBuffers == 2 ? 1024 : (kConeWgsPerCu == 2 ? 512 : 256);
+constexpr int kConeBlock = 64 * RT_CONE_WAVES;
 static_assert(kConeBlock % 64 == 0, "whole waves");
 constexpr int kConeWaves = kConeBlock / 64;
 constexpr int kConeWavesPerSimd = kConeWgsPerCu * kConeWaves / 4;
-constexpr int kLdsBufFloats = kConeBuffers == 2 ? 17920 : (kConeWgsPerCu == 2 ? 18176 : (kConeWgsPerCu == 3 ? 11712 : 8704));   // one level buffer: a unit's fill (16-byte chunks, runs per range)
+constexpr int kLdsBufFloats = 18176;        // one level buffer: a unit's fill (16-byte chunks, runs per range)
 constexpr int kLdsDataFloats = kLdsBufFloats - 256;   // rows x p of any level (the rest: per-range 16-byte phase slack)
 constexpr int kLdsPadFloats = 128;          // slack read (never used) by the unused slots of the last row
-constexpr int kMaxRows = kConeWgsPerCu == 4 ? 192 : (kConeWgsPerCu == 3 ? 256 : 384);          // rows per level (row-offset table, descriptors)
-constexpr int kDescEntries = kConeWgsPerCu == 4 ? 512 : (kConeWgsPerCu == 3 ? 768 : 1024);     // row-descriptor table (all levels of a unit)
+constexpr int kMaxRows = 384;               // rows per level (row-offset table, descriptors)
+constexpr int kDescEntries = 1024;          // row-descriptor table (all levels of a unit)
 constexpr int kMaxTileLevels = 6;           // L for tile items
 constexpr int kMaxLevels = 11;              // merge levels of any unit (whole units: ceil(log2(kMaxRows)))
 constexpr int kMaxRanges = (1 << (kMaxTileLevels + 1)) - 1;
@@ -66,18 +54,12 @@ constexpr int kSnrChunk = 17;               // S/N epilogue: columns per lane he
 // S/N epilogue (ffa_kernels.hip snr_rows): widths <= kSnrWin from a
 // register window; chunk columns per lane of the register-window path
 constexpr int kSnrWin = 12;
-#ifndef RT_SNR_MAX_CHUNK
-#define RT_SNR_MAX_CHUNK 17
-#endif
-constexpr int kSnrMaxChunk = RT_SNR_MAX_CHUNK;
+constexpr int kSnrMaxChunk = 17;
 // Widths past the register window as plain LDS windows: a final level whose
 // row stride holds the wrapped prefix c[p + e] = c[e] + sum for e < wmax
 // after each row, so every lane's column j0 + t + w (t < its chunk) is a
 // plain read (the planner caps final tiles so their rows fit at this stride:
-// plan.cpp final_tile_cap).  A/B: DESIGN.md section 3.1.
-#ifndef RT_SNR_WIDE_EXT
-#define RT_SNR_WIDE_EXT 1
-#endif
+// plan.cpp final_tile_cap).
 RT_HD inline int snr_wide_stride(int p, int wmax)
 {
     return p + (wmax > kSnrMaxChunk ? wmax : kSnrMaxChunk);
@@ -95,7 +77,7 @@ RT_HD constexpr int snr_group(int p)
     while (G < 64 && ((((p + G - 1) / G) | 1) > kSnrMaxChunk)) G <<= 1;
     return G;
 }
-constexpr int kStageRegs = kConeBuffers == 2 ? 25 : (kConeWgsPerCu == 3 ? 60 : 45);   // merge: staged values per lane (rows x slots)
+constexpr int kStageRegs = 45 * 8 / RT_CONE_WAVES;   // merge: staged values per lane (rows x slots)
 constexpr int kMaxSlots = 45;               // merge: 64-bin slots per row (p <= 2880)
 constexpr int kMaxRowsPerWave = 24;         // merge: staged rows per wave
 // header words of a unit's host-built blob (plan.hpp build_tile_blob); a
@@ -121,10 +103,7 @@ enum : uint32_t { kSlotOne = 0, kSlotTwo = 1, kSlotPair = 2, kSlotHalf = 3 };
 // (the level-l+1 head row H', or H for a single step) is computed once for
 // both and only row B's tail term is read (RT_SLOT_HALF: the planner emits
 // them; the kernel always runs them)
-#ifndef RT_SLOT_HALF
-#define RT_SLOT_HALF 1
-#endif
-constexpr int kSlotWords = kConeWgsPerCu == 4 ? 288 : 544;   // LDS area of a unit's slot tables
+constexpr int kSlotWords = 544;             // LDS area of a unit's slot tables
 // 4/5-slot variants (p = 193-320, rows <= 72 per unit): slot tables with
 // every row resolved (build_tile_blob), 16 bytes per row: source-row LDS
 // offsets (16 bits each), the three rolls (10 bits each, | carried << 30 for
@@ -135,9 +114,6 @@ constexpr int kAuxMetaWords = kBlobHeader + kDescEntries + kMaxRows + kSlotWords
 // x < 256 + 64 at the end of the metadata area, which it extends by kLutPad
 // words (the workgroup's LDS stays inside the same 512-byte granule); every
 // 4-slot row-slot unit's blob LDS part must end at or before kLut4Off
-#ifndef RT_ROLL_LUT
-#define RT_ROLL_LUT 1
-#endif
 constexpr int kLutPad = 64;
 constexpr int kLut4Words = 2 * (256 + 64);
 constexpr int kLut4Off = kAuxMetaWords + kLutPad - kLut4Words;
@@ -155,16 +131,14 @@ RT_HD inline int fill_chunks_bound(int n, int p, int runs) { return (n * p + 6 *
 RT_HD inline int pack_blob_words(int entries, int nb) { return (kBlobHeader + entries + nb + 2 * kMaxLevels + 4) & ~3; }
 
 // Merge variant for rows of p phase bins: slots per row rounded up to an
-// instantiated width (1..5, 8, 16, 45), or kPack2 for p <= 32 (two rows per
-// wave instruction, lanes 0-31 and 32-63); 0 if p is too wide for the LDS
-// engine.  The value is the cone kernel's template argument and launch bucket.
-#ifndef RT_PACK_SMALL_ROWS
-#define RT_PACK_SMALL_ROWS 1
-#endif
+// instantiated width (1..5, 8, 16, 45), or kPack2 for p <= 32 (short rows:
+// (row, 8-bin segment) tasks, ffa_kernels.hip merge_step_tasks); 0 if p is
+// too wide for the LDS engine.  The value is the cone kernel's template
+// argument and launch bucket.
 constexpr int kPack2 = 64;
 RT_HD inline int merge_slots(uint32_t p)
 {
-    if (RT_PACK_SMALL_ROWS && p <= 32) return kPack2;
+    if (p <= 32) return kPack2;
     if (p == 0) return 1;
     const int s = (int)((p + 63) / 64);
     if (s <= 5) return s;
@@ -174,28 +148,21 @@ RT_HD inline int merge_slots(uint32_t p)
     return 0;
 }
 
-// 64-lane slots per register row of a merge variant, and rows per slot
 // Row stride of the merge levels above the fill in the short-row variant
 // (kPack2, ffa_kernels.hip merge_step_tasks): odd for p >= 8.
-#ifndef RT_PACK_TASKS
-#define RT_PACK_TASKS 1
-#endif
-RT_HD inline int pack_stride(int p) { return RT_PACK_TASKS && p >= 8 ? (p | 1) : p; }
+RT_HD inline int pack_stride(int p) { return p >= 8 ? (p | 1) : p; }
+// 64-lane slots per register row of a merge variant, and rows per slot
 RT_HD constexpr int slot_count(int smax) { return smax == kPack2 ? 1 : smax; }
 RT_HD constexpr int row_pack(int smax) { return smax == kPack2 ? 2 : 1; }
 
 // Register rows per wave the merge stages for a variant (register budget);
-// each register row holds row_pack(smax) output rows.
-// register rows per wave of the 4-slot variant: its LDS capacity at p >= 221
-// (5 x 16 waves = 80 >= 17664 / 221) or at p >= 240 (9 x 8 waves = 72 >=
-// 16128 / 240)
-#ifndef RT_RW4
-#define RT_RW4 (kConeBuffers == 2 ? 5 : (kConeWgsPerCu == 3 ? 12 : 9))
-#endif
+// each register row holds row_pack(smax) output rows.  The 4-slot variant
+// stages 9: its LDS capacity at p >= 240 (9 x 8 waves = 72 >= 16128 / 240).
+constexpr int kRw4 = (72 + RT_CONE_WAVES - 1) / RT_CONE_WAVES;
 RT_HD constexpr int merge_rows_per_wave(int smax)
 {
-    return (smax == 4 && RT_RW4 > 0)
-               ? RT_RW4
+    return smax == 4
+               ? kRw4
                : (kStageRegs / slot_count(smax) < 1
                       ? 1
                       : (kStageRegs / slot_count(smax) < kMaxRowsPerWave ? kStageRegs / slot_count(smax)
@@ -257,7 +224,6 @@ enum : uint32_t {
     kConeDiagNoBarrier = 1u << 27, // diagnostics only (wrong results): no barriers between merge levels
     kConeDiagNoLand = 1u << 26,  // diagnostics only (wrong results): fill loads issued but not landed in LDS
     kConeDiagNoDesc = 1u << 25,  // diagnostics only (wrong results): no descriptor table
-    kConeDiagExitWait = 1u << 24, // A/B only: wait for the unit's stores before the workgroup ends
     kConeDiagNoFill = 1u << 23,  // diagnostics only (wrong results): metadata DMA only, no bottom-level fill
     kConeDefaultFeatures = 7u   // kConeSnrStride: final-pass rows at a stride with room for the S/N wrap extension
 };

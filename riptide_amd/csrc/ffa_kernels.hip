@@ -237,15 +237,7 @@ hipError_t launch_downsample_ladder(const float* x, uint64_t n_in, uint64_t x_st
 // stores (64 consecutive words per wave instruction) are nt: the short-row
 // stores (4-byte scattered per lane) took cfg4 from 0.776 to 1.306 ms per
 // trial with nt (r03zh_ab_cfg4.log) and keep the default.
-#ifndef RT_FILL_CPOL
-#define RT_FILL_CPOL 0
-#endif
-#ifndef RT_STORE_CPOL
-#define RT_STORE_CPOL 2
-#endif
-#ifndef RT_SNR_CPOL
-#define RT_SNR_CPOL 0
-#endif
+constexpr int kFillCpol = 0, kStoreCpol = 2, kSnrCpol = 0;
 
 // LDS-only workgroup barrier: orders LDS accesses without waiting for the
 // global loads or stores that are still in flight.
@@ -375,7 +367,7 @@ __device__ __forceinline__ void dma_run(__amdgpu_buffer_rsrc_t rs, uint32_t goff
         const int c = c0 + lane;
         if (c < nch)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds + 4 * c0), 16,
-                                                     (int)(goff + 16u * (uint32_t)c), 0, 0, RT_FILL_CPOL);
+                                                     (int)(goff + 16u * (uint32_t)c), 0, 0, kFillCpol);
     }
 }
 
@@ -443,7 +435,7 @@ __device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t u, uin
         } else {
             ok = ok && C.nb <= cap && C.entries <= kDescEntries && words <= kAuxWords;
             // the 4-slot roll table lies past the blob's LDS part
-            if (SMAX == 4 && RT_ROLL_LUT && C.slots) ok = ok && words <= kLut4Off;
+            if (SMAX == 4 && C.slots) ok = ok && words <= kLut4Off;
         }
         ok = ok && words >= kBlobHeader + C.entries + C.nb && C.nruns <= 64 * kConeWaves && (words & 3) == 0;
 #ifdef RT_STAMPS
@@ -467,7 +459,7 @@ __device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t u, uin
                 const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)sv.z, i);
                 if (lane < n && 4 * (c0 + n) <= kLdsBufFloats && !(a.flags & kConeDiagNoFill))
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(buf + 4 * c0),
-                                                             16, (int)((g + (uint32_t)lane) * 16u), 0, 0, RT_FILL_CPOL);
+                                                             16, (int)((g + (uint32_t)lane) * 16u), 0, 0, kFillCpol);
             }
         }
     }
@@ -542,21 +534,6 @@ typedef const __attribute__((address_space(3))) float* lds_cptr;
 // LDS reads the compiler must not pair into ds_read2_b32 / ds_read2st64_b32
 // (those issue at a lower rate than separate ds_read_b32 on gfx950,
 // tools/microbench/lds_b64.hip): volatile accesses are never merged.
-#ifndef RT_MERGE_PIPE
-#define RT_MERGE_PIPE 0
-#endif
-#ifndef RT_SLOT_OPAQUE_LANE
-#define RT_SLOT_OPAQUE_LANE 0
-#endif
-// A/B knobs of the row-slot merge (measured, ms per cfg2 trial): a template
-// constant instead of the run-time loff test in the slot resolution 8.96 vs
-// 8.81 (the second instance of the slot loop costs more than the branches it
-// removes; kept off -- the short-row path, whose branches sat in its row
-// loop, gained: cfg4 1.64 -> 1.40); an opaque lane copy per step 9.04.
-#ifndef RT_SLOT_FIRST
-#define RT_SLOT_FIRST 0
-#endif
-
 __device__ __forceinline__ float lds_ld(lds_cptr p) { return *(const volatile __attribute__((address_space(3))) float*)p; }
 
 // Outputs of level l (rows wave + 8i) into v, from the level below in dense
@@ -653,46 +630,6 @@ __device__ __forceinline__ void merge_level2_dense(const UnitCtx& C, const float
         s3 = sTT;
     }
     const lds_cptr l1 = (lds_cptr)src + lane;
-#if RT_MERGE_PIPE
-    if constexpr (SMAX <= 5) {
-        // software-pipelined rows: the reads of row i + 1 are issued before
-        // the additions of row i, so a wave keeps up to 4 SMAX LDS reads in
-        // flight across the row boundary instead of draining per row
-        float x[2][SMAX][4];
-        auto issue = [&](int i, float (&xx)[SMAX][4]) {
-            const lds_cptr hrow = l1 + __builtin_amdgcn_readlane(o0, i);
-            lds_cptr b1 = l1 + __builtin_amdgcn_readlane(o1, i);
-            lds_cptr b2 = l1 + __builtin_amdgcn_readlane(o2, i);
-            lds_cptr b3 = l1 + __builtin_amdgcn_readlane(o3, i);
-            lds_cptr w1 = b1 - p, w2 = b2 - p, w3 = b3 - p;
-            asm("" : "+v"(b1), "+v"(w1), "+v"(b2), "+v"(w2), "+v"(b3), "+v"(w3));
-            const int ls1 = lane + __builtin_amdgcn_readlane(s1, i);
-            const int ls2 = lane + __builtin_amdgcn_readlane(s2, i);
-            const int ls3 = lane + __builtin_amdgcn_readlane(s3, i);
-#pragma unroll
-            for (int k = 0; k < SMAX; ++k) {
-                const int wk = p - 64 * k;
-                xx[k][0] = hrow[64 * k];
-                xx[k][1] = lds_ld((ls1 >= wk ? w1 : b1) + 64 * k);
-                xx[k][2] = lds_ld((ls2 >= wk ? w2 : b2) + 64 * k);
-                xx[k][3] = lds_ld((ls3 >= wk ? w3 : b3) + 64 * k);
-            }
-        };
-        issue(0, x[0]);
-#pragma unroll
-        for (int i = 0; i < RW; ++i) {
-            if (i + 1 < RW) issue(i + 1, x[(i + 1) & 1]);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int k = 0; k < SMAX; ++k) {
-                const float(&y)[4] = x[i & 1][k];
-                v[i][k] = __fadd_rn(__fadd_rn(y[0], y[1]), __fadd_rn(y[2], y[3]));
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        return;
-    }
-#endif
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
         const lds_cptr hrow = l1 + __builtin_amdgcn_readlane(o0, i);
@@ -737,10 +674,10 @@ __device__ __forceinline__ void store_rows(const float (&v)[RW][SMAX], int p, in
                     // store out of the buffer's range, which drops them
                     const uint32_t o = k < SMAX - 1 ? ob + 256u * (uint32_t)k
                                                     : (tail_ok ? ob + 256u * (uint32_t)k : 0x80000000u);
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs, (int)o, 0, RT_STORE_CPOL);
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs, (int)o, 0, kStoreCpol);
                 } else if (64 * (k + 1) <= p || (k < S && lane + 64 * k < p)) {
                     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs,
-                                                          (int)(ob + 256u * (uint32_t)k), 0, RT_STORE_CPOL);
+                                                          (int)(ob + 256u * (uint32_t)k), 0, kStoreCpol);
                 }
             }
         }
@@ -786,45 +723,6 @@ __device__ __forceinline__ void write_rows(float* base, float* dummy, const floa
 // lane 63 from lane 0 of the next slot, and bin p - 1 from bin 0.  Half the
 // LDS reads of the pair.
 //
-// A rolled row read with a wave-uniform wrap slot (RT_WRAP_BRANCH): bins
-// j = lane + 64k of the row at roll t read T[(j + t) mod p].  With
-// K = (p - t) >> 6, every lane of slot k < K reads before the wrap point and
-// every lane of slot k > K after it; only slot K straddles it.  One uniform
-// branch on K (SGPR) picks code in which slots below K read base b, slots
-// above K base b - p, and slot K alone selects per lane: 2 VALU per rolled
-// row instead of a compare and a select per slot.  Same LDS words, same
-// results.  A/B knob, off: cone ms per cfg2 trial 8.65 vs 7.79 with it (the
-// compiler linearises the uniform branches and waits for every case's reads
-// at each join, profiles/r03q_ab_*.log).
-#ifndef RT_WRAP_BRANCH
-#define RT_WRAP_BRANCH 0
-#endif
-template <int SMAX, int KC>
-__device__ __forceinline__ void rolled_case(lds_cptr b, lds_cptr w, int ls, int p, float (&x)[SMAX])
-{
-#pragma unroll
-    for (int k = 0; k < SMAX; ++k) {
-        if (k < KC) x[k] = lds_ld(b + 64 * k);
-        else if (k == KC) x[k] = lds_ld((ls >= p - 64 * k ? w : b) + 64 * k);
-        else x[k] = lds_ld(w + 64 * k);
-    }
-}
-template <int SMAX>
-__device__ __forceinline__ void rolled_row(lds_cptr b, int p, int lane, int t, float (&x)[SMAX])
-{
-    lds_cptr w = b - p;
-    asm("" : "+v"(b), "+v"(w));
-    const int ls = lane + t;
-    const int K = (p - t) >> 6;
-    static_assert(SMAX >= 1 && SMAX <= 5, "wrap-slot cases");
-    if (K <= 0) rolled_case<SMAX, 0>(b, w, ls, p, x);
-    else if (SMAX > 1 && K == 1) rolled_case<SMAX, 1>(b, w, ls, p, x);
-    else if (SMAX > 2 && K == 2) rolled_case<SMAX, 2>(b, w, ls, p, x);
-    else if (SMAX > 3 && K == 3) rolled_case<SMAX, 3>(b, w, ls, p, x);
-    else if (SMAX > 4 && K == 4) rolled_case<SMAX, 4>(b, w, ls, p, x);
-    else rolled_case<SMAX, SMAX>(b, w, ls, p, x);   // p - t >= 64 SMAX: no wrap
-}
-
 // Per-row terms from the row's scalars (SGPRs): r0 head row offset, r1..r3
 // the rolled rows' offsets (+ their rolls), t1..t3 the rolls, c1 carried.
 // HEAD false (row B of a kSlotHalf): only the tail term; hs is row A's.
@@ -832,37 +730,6 @@ template <int SMAX, bool TWO, bool HEAD = true>
 __device__ __forceinline__ void row_terms_s(lds_cptr l1, int p, int lane, int r0, int r1, int r2, int r3, int t1,
                                             int t2, int t3, int c1, float (&hs)[SMAX], float (&ts)[SMAX])
 {
-#if RT_WRAP_BRANCH
-    if constexpr (SMAX <= 5) {
-        if constexpr (TWO) {
-            float x1[SMAX], x2[SMAX], x3[SMAX];
-            if constexpr (HEAD) rolled_row<SMAX>(l1 + r1, p, lane, t1, x1);
-            rolled_row<SMAX>(l1 + r2, p, lane, t2, x2);
-            rolled_row<SMAX>(l1 + r3, p, lane, t3, x3);
-#pragma unroll
-            for (int k = 0; k < SMAX; ++k) {
-                if constexpr (HEAD) hs[k] = __fadd_rn(lds_ld(l1 + r0 + 64 * k), x1[k]);
-                ts[k] = __fadd_rn(x2[k], x3[k]);
-            }
-        } else {
-            float x[SMAX];
-            rolled_row<SMAX>(l1 + r1, p, lane, t1, x);
-            if constexpr (HEAD) {
-                const uint32_t keep = c1 ? 0u : 0xFFFFFFFFu;
-                const uint32_t neg0 = ~keep & 0x80000000u;
-#pragma unroll
-                for (int k = 0; k < SMAX; ++k) {
-                    hs[k] = lds_ld(l1 + r0 + 64 * k);
-                    ts[k] = __uint_as_float((__float_as_uint(x[k]) & keep) | neg0);
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < SMAX; ++k) ts[k] = x[k];
-            }
-        }
-        return;
-    }
-#endif
     if constexpr (TWO && !HEAD) {
         lds_cptr b2 = l1 + r2;
         lds_cptr b3 = l1 + r3;
@@ -923,7 +790,7 @@ __device__ __forceinline__ void row_terms_s(lds_cptr l1, int p, int lane, int r0
     }
 }
 
-// Roll table (RT_ROLL_LUT, 4-slot rows, p = 193..256): a rolled read of a
+// Roll table (4-slot rows, p = 193..256): a rolled read of a
 // row at roll t takes bin j = lane + 64k from T[(lane + t + 64k) mod p].
 // Entry x = lane + t (x < p + 64) of a per-unit LDS table holds the four
 // byte offsets 4 ((x + 64k) mod p), k = 0..3, as 16-bit halves of 8 bytes:
@@ -933,13 +800,6 @@ __device__ __forceinline__ void row_terms_s(lds_cptr l1, int p, int lane, int r0
 // point.  Same LDS words, same additions: bit-exact.  The table sits at the
 // end of the unit's metadata area (kLut4Off, past every blob's LDS part:
 // validate_exec_plan) and is rebuilt by every unit of a 4-slot instance.
-// roll-table entries of row A read one slot ahead (merge_step_slots).  A/B
-// knob, off: neutral (cone ms per trial cfg2 7.69 / 7.68 with it vs 7.70 /
-// 7.68, profiles/r03w_ab_*.log) -- the table's round trip was not on the
-// critical path
-#ifndef RT_LUT_AHEAD
-#define RT_LUT_AHEAD 0
-#endif
 typedef const __attribute__((address_space(3))) unsigned long long* lut_cptr;
 typedef const __attribute__((address_space(3))) char* lds_ccptr;
 
@@ -961,14 +821,12 @@ __device__ __forceinline__ void rolled_lut4(lds_ccptr rb, unsigned long long e, 
 // head reads are in flight while the entries return.
 template <bool TWO, bool HEAD = true>
 __device__ __forceinline__ void row_terms_lut(lds_cptr l1, lds_cptr s0, lut_cptr lutl, int r0, int q1, int q2, int q3,
-                                              int t1, int t2, int t3, int c1, float (&hs)[4], float (&ts)[4],
-                                              const unsigned long long* pre = nullptr)
+                                              int t1, int t2, int t3, int c1, float (&hs)[4], float (&ts)[4])
 {
     const lds_ccptr b = (lds_ccptr)s0;
     if constexpr (TWO) {
-        // pre: the row's three entries, read one slot ahead (merge_step_slots)
-        const unsigned long long e1 = pre ? pre[0] : (HEAD ? lutl[t1] : 0ull);
-        const unsigned long long e2 = pre ? pre[1] : lutl[t2], e3 = pre ? pre[2] : lutl[t3];
+        const unsigned long long e1 = HEAD ? lutl[t1] : 0ull;
+        const unsigned long long e2 = lutl[t2], e3 = lutl[t3];
         float h[4], x1[4], x2[4], x3[4];
         if constexpr (HEAD) {
 #pragma unroll
@@ -983,7 +841,7 @@ __device__ __forceinline__ void row_terms_lut(lds_cptr l1, lds_cptr s0, lut_cptr
             ts[k] = __fadd_rn(x2[k], x3[k]);
         }
     } else {
-        const unsigned long long e = pre ? pre[0] : lutl[t1];
+        const unsigned long long e = lutl[t1];
         float x[4];
         if constexpr (HEAD) {
 #pragma unroll
@@ -1025,10 +883,9 @@ __device__ __forceinline__ void build_roll_lut4(uint32_t* lut, int p, int tid)
 template <int SMAX, bool TWO, bool HEAD = true>
 __device__ __forceinline__ void row_terms(lds_cptr l1, int p, int lane, int i, int o0, int o1, int o2, int o3, int s1,
                                           int s2, int s3, float (&hs)[SMAX], float (&ts)[SMAX],
-                                          lds_cptr s0 = nullptr, lut_cptr lutl = nullptr,
-                                          const unsigned long long* pre = nullptr)
+                                          lds_cptr s0 = nullptr, lut_cptr lutl = nullptr)
 {
-    if constexpr (SMAX == 4 && RT_ROLL_LUT) {
+    if constexpr (SMAX == 4) {
         // o1 .. o3 are the rolled rows' offsets without their rolls here
         if constexpr (TWO) {
             if constexpr (HEAD) {
@@ -1037,7 +894,7 @@ __device__ __forceinline__ void row_terms(lds_cptr l1, int p, int lane, int i, i
                 int t1 = __builtin_amdgcn_readlane(s1, i), t2 = __builtin_amdgcn_readlane(s2, i);
                 int t3 = __builtin_amdgcn_readlane(s3, i);
                 asm volatile("" : "+s"(r0), "+s"(q1), "+s"(q2), "+s"(q3), "+s"(t1), "+s"(t2), "+s"(t3));
-                row_terms_lut<true>(l1, s0, lutl, r0, q1, q2, q3, t1, t2, t3, 0, hs, ts, pre);
+                row_terms_lut<true>(l1, s0, lutl, r0, q1, q2, q3, t1, t2, t3, 0, hs, ts);
             } else {
                 int q2 = __builtin_amdgcn_readlane(o2, i), q3 = __builtin_amdgcn_readlane(o3, i);
                 int t2 = __builtin_amdgcn_readlane(s2, i), t3 = __builtin_amdgcn_readlane(s3, i);
@@ -1049,7 +906,7 @@ __device__ __forceinline__ void row_terms(lds_cptr l1, int p, int lane, int i, i
                 int r0 = __builtin_amdgcn_readlane(o0, i), q1 = __builtin_amdgcn_readlane(o1, i);
                 int t1 = __builtin_amdgcn_readlane(s1, i), c1 = __builtin_amdgcn_readlane(o2, i);
                 asm volatile("" : "+s"(r0), "+s"(q1), "+s"(t1), "+s"(c1));
-                row_terms_lut<false>(l1, s0, lutl, r0, q1, 0, 0, t1, 0, 0, c1, hs, ts, pre);
+                row_terms_lut<false>(l1, s0, lutl, r0, q1, 0, 0, t1, 0, 0, c1, hs, ts);
             } else {
                 int q1 = __builtin_amdgcn_readlane(o1, i), t1 = __builtin_amdgcn_readlane(s1, i);
                 asm volatile("" : "+s"(q1), "+s"(t1));
@@ -1088,52 +945,19 @@ __device__ __forceinline__ void row_terms(lds_cptr l1, int p, int lane, int i, i
     }
 }
 
-// The same from a lane's packed 16-byte resolved entry (e.x: head row | first
-// rolled row << 16, e.y: the other two rolled rows, e.z: the three rolls,
-// carried bit 30): three v_readlane per row, the unpacking in scalar code.
-// A/B knob, off: same box, cone ms per cfg2 trial 7.97 / 7.95 with it vs
-// 7.61 / 7.64 without (the scalar unpacking costs more than the four
-// v_readlane it saves).
-#ifndef RT_PACKED_READLANE
-#define RT_PACKED_READLANE 0
-#endif
-template <int SMAX, bool TWO>
-__device__ __forceinline__ void row_terms_packed(lds_cptr l1, int p, int lane, int i, uint32_t ex, uint32_t ey,
-                                                 uint32_t ez, float (&hs)[SMAX], float (&ts)[SMAX])
-{
-    uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)ex, i);
-    uint32_t z = (uint32_t)__builtin_amdgcn_readlane((int)ez, i);
-    if constexpr (TWO) {
-        uint32_t y = (uint32_t)__builtin_amdgcn_readlane((int)ey, i);
-        asm volatile("" : "+s"(x), "+s"(y), "+s"(z));
-        const int t1 = (int)(z & 1023u), t2 = (int)((z >> 10) & 1023u), t3 = (int)((z >> 20) & 1023u);
-        row_terms_s<SMAX, true>(l1, p, lane, (int)(x & 0xFFFFu), (int)(x >> 16) + t1, (int)(y & 0xFFFFu) + t2,
-                                (int)(y >> 16) + t3, t1, t2, t3, 0, hs, ts);
-    } else {
-        asm volatile("" : "+s"(x), "+s"(z));
-        const int t1 = (int)(z & 1023u);
-        row_terms_s<SMAX, false>(l1, p, lane, (int)(x & 0xFFFFu), (int)(x >> 16) + t1, 0, 0, t1, 0, 0,
-                                 (int)((z >> 30) & 1u), hs, ts);
-    }
-}
-
-template <int SMAX, int RW, bool TWO, bool FIRST>
+template <int SMAX, int RW, bool TWO>
 __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* src, int p, int lo, int lane,
                                                  int wave, float (&v)[RW][SMAX], const int* loff, uint32_t& sw,
                                                  int& nq)
 {
     constexpr int Q = (RW + 1) / 2;
     static_assert(Q <= 32, "row slots: one lane per slot row");
-#if RT_SLOT_OPAQUE_LANE
-    asm volatile("" : "+v"(lane));
-#endif
     const uint32_t* st = slot_table(C, lo);
     const int ns = uni((int)st[0]);
     nq = uni(ns > wave ? (ns - wave + kConeWaves - 1) / kConeWaves : 0);
     // lane i < 32 resolves row A of the wave's slot i, lane 32 + i its row B
     const int qi = lane & 31;
     int o0 = 0, o1 = 0, o2 = 0, o3 = 0, s1 = 0, s2 = 0, s3 = 0;
-    uint32_t ex = 0, ey = 0, ez = 0;      // the packed entry (RT_PACKED_READLANE)
     if constexpr (resolved_slots(SMAX)) {
         // host-resolved rows: one 16-byte entry per lane (the slot's row A in
         // lanes 0-31 with the slot word, row B in lanes 32-63)
@@ -1142,12 +966,9 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
         const int qc = qi < Q ? qi : Q - 1;
         const uint4 e = reinterpret_cast<const uint4*>(st)[1 + (lane >> 5) * (kConeWaves * Q) + wave * Q + qc];
         sw = lane < 32 ? e.w : 0u;
-        ex = e.x;
-        ey = e.y;
-        ez = e.z;
         s1 = (int)(e.z & 1023u);
         // the roll table path takes the rolled rows' offsets without rolls
-        constexpr int roll_in = SMAX == 4 && RT_ROLL_LUT ? 0 : 1;
+        constexpr int roll_in = SMAX == 4 ? 0 : 1;
         if constexpr (TWO) {
             s2 = (int)((e.z >> 10) & 1023u);
             s3 = (int)((e.z >> 20) & 1023u);
@@ -1166,9 +987,8 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
     const bool act = qi < nq && (lane < 32 || (sw >> 20) == kSlotTwo || (sw >> 20) == kSlotHalf);
     const int r = lane < 32 ? (int)(sw & 1023u) : (int)((sw >> 10) & 1023u);
     const uint32_t* const desc = desc_table(C);
-    // the first step reads the bottom level through its row offsets: a
-    // template constant (a run-time test of loff made every offset a branch)
-    const bool use_loff = RT_SLOT_FIRST ? FIRST : loff != nullptr;
+    // the first step reads the bottom level through its row offsets
+    const bool use_loff = loff != nullptr;
     if (act) {
         if constexpr (TWO) {
             const uint32_t d0 = desc[desc_offset(C, lo) + r];
@@ -1199,33 +1019,12 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
     const lds_cptr s0 = (lds_cptr)src;
     const lut_cptr lutl = (lut_cptr)(C.aux0 + kLut4Off) + lane;
     const int jl = p - 1 - 64 * (SMAX - 1);   // lane of bin p - 1 in the last slot
-    // roll table: row A's table entries are read one slot ahead (their LDS
-    // round trip overlaps the previous slot's reads); slots past nq read
-    // valid entries of their lanes' clamped rows and are never used
-    constexpr bool PRE = SMAX == 4 && RT_ROLL_LUT && RT_LUT_AHEAD;
-    unsigned long long pe[3] = {0ull, 0ull, 0ull};
-    auto lut_ahead = [&](int q) {
-        if constexpr (PRE) {
-            pe[0] = lutl[__builtin_amdgcn_readlane(s1, q)];
-            if constexpr (TWO) {
-                pe[1] = lutl[__builtin_amdgcn_readlane(s2, q)];
-                pe[2] = lutl[__builtin_amdgcn_readlane(s3, q)];
-            }
-        }
-    };
-    lut_ahead(0);
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
         if (q < nq) {
             const uint32_t kq = (uint32_t)__builtin_amdgcn_readlane((int)sw, q) >> 20;
             float hs[SMAX], ts[SMAX];
-            if constexpr (resolved_slots(SMAX) && RT_PACKED_READLANE) {
-                row_terms_packed<SMAX, TWO>(l1, p, lane, q, ex, ey, ez, hs, ts);
-            } else {
-                unsigned long long cur[3] = {pe[0], pe[1], pe[2]};
-                if (q + 1 < Q) lut_ahead(q + 1);
-                row_terms<SMAX, TWO>(l1, p, lane, q, o0, o1, o2, o3, s1, s2, s3, hs, ts, s0, lutl, PRE ? cur : nullptr);
-            }
+            row_terms<SMAX, TWO>(l1, p, lane, q, o0, o1, o2, o3, s1, s2, s3, hs, ts, s0, lutl);
 #pragma unroll
             for (int k = 0; k < SMAX; ++k) v[2 * q][k] = __fadd_rn(hs[k], ts[k]);
             const int qb = 2 * q + 1 < RW ? 2 * q + 1 : RW - 1;   // row B's register row (q < Q: in range)
@@ -1248,10 +1047,7 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
 #pragma unroll
                     for (int k = 0; k < SMAX; ++k) v[qb][k] = __fadd_rn(hs[k], tb[k]);
                 } else if (kq == kSlotTwo) {
-                    if constexpr (resolved_slots(SMAX) && RT_PACKED_READLANE)
-                        row_terms_packed<SMAX, TWO>(l1, p, lane, 32 + q, ex, ey, ez, hs, ts);
-                    else
-                        row_terms<SMAX, TWO>(l1, p, lane, 32 + q, o0, o1, o2, o3, s1, s2, s3, hs, ts, s0, lutl);
+                    row_terms<SMAX, TWO>(l1, p, lane, 32 + q, o0, o1, o2, o3, s1, s2, s3, hs, ts, s0, lutl);
 #pragma unroll
                     for (int k = 0; k < SMAX; ++k) v[qb][k] = __fadd_rn(hs[k], ts[k]);
                 }
@@ -1260,37 +1056,14 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
     }
 }
 
-// final-pass rows zero-padded past p for unmasked S/N chunk reads (A/B knob):
-// 1 = zeros up to the row stride (same box, cone ms per cfg2 trial 7.98 /
-// 7.97 with it vs 7.86 / 7.81 without -- the merge's extra zero stores and
-// the second S/N read path cost more than the 17 column selects per row pass
-// they save); 2 = zeros only from the last slot's lanes past p, which store
-// anyway (no extra store), where every chunk up to the row's owner ends
-// inside the slots (cfg2 7.58 / 7.61 with it vs 7.53 / 7.48, cfg3 1.90 vs
-// 1.88: the 17 masking selects it removes sat in the shadow of the serial
-// fp64 prefix chain; profiles/r03z_ab_*.log)
-#ifndef RT_SNR_ZPAD
-#define RT_SNR_ZPAD 0
-#endif
-
 // Slot-step write-back into the dense LDS rows at base / store to global
 // memory (a non-final pass's output level): register rows 2q, 2q + 1 to the
-// slot's rows A and B.
-// zpad (a final pass's output level at the S/N stride q): the bins past p
-// up to q are written as +0.0, so the S/N reads its chunks without masking
-// the columns past the row (adding +0.0 to its fp64 partial sums is exact).
+// slot's rows A and B (row stride q: p, or a final pass's S/N stride).
 template <int SMAX, int RW>
 __device__ __forceinline__ void write_rows_slots(float* base, float* dummy, const float (&v)[RW][SMAX], int p,
-                                                 int lane, uint32_t sw, int nq, int q, bool zpad = false)
+                                                 int lane, uint32_t sw, int nq, int q)
 {
-#if RT_SLOT_OPAQUE_LANE
-    asm volatile("" : "+v"(lane));
-#endif
     const bool tail_ok = lane + 64 * (SMAX - 1) < p;
-    // zpad: the last slot's lanes past p store +0.0 at their own bin (when it
-    // lies inside the stride), and lanes past 64 SMAX clear the rest of it
-    const bool tail_zero = zpad && !tail_ok && lane + 64 * (SMAX - 1) < q;
-    const bool rest_zero = zpad && lane + 64 * SMAX < q;
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
         if (i / 2 < nq) {
@@ -1301,9 +1074,8 @@ __device__ __forceinline__ void write_rows_slots(float* base, float* dummy, cons
 #pragma unroll
                 for (int k = 0; k < SMAX; ++k) {
                     if (k < SMAX - 1) orow[64 * k] = v[i][k];
-                    else *((tail_ok || tail_zero) ? orow + 64 * k : dummy) = tail_ok ? v[i][k] : 0.0f;
+                    else *(tail_ok ? orow + 64 * k : dummy) = v[i][k];
                 }
-                if (RT_SNR_ZPAD == 1 && zpad && 64 * SMAX < q) *(rest_zero ? orow + 64 * SMAX : dummy) = 0.0f;
             }
         }
     }
@@ -1313,9 +1085,6 @@ template <int SMAX, int RW>
 __device__ __forceinline__ void store_rows_slots(const float (&v)[RW][SMAX], int p, int lane, uint32_t sw, int nq,
                                                  __amdgpu_buffer_rsrc_t rs, uint32_t st_o0)
 {
-#if RT_SLOT_OPAQUE_LANE
-    asm volatile("" : "+v"(lane));
-#endif
     const bool tail_ok = lane + 64 * (SMAX - 1) < p;
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
@@ -1328,7 +1097,7 @@ __device__ __forceinline__ void store_rows_slots(const float (&v)[RW][SMAX], int
                 for (int k = 0; k < SMAX; ++k) {
                     const uint32_t o = k < SMAX - 1 ? ob + 256u * (uint32_t)k
                                                     : (tail_ok ? ob + 256u * (uint32_t)k : 0x80000000u);
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs, (int)o, 0, RT_STORE_CPOL);
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs, (int)o, 0, kStoreCpol);
                 }
             }
         }
@@ -1363,10 +1132,7 @@ __device__ __forceinline__ void merge_step_lanes(const UnitCtx& C, const float* 
     const lds_cptr sp = (lds_cptr)src;
     // groups of G register rows without a branch between them, so the
     // descriptor chains (2-4 dependent LDS reads per row) of a group overlap
-#ifndef RT_LANES_GROUP
-#define RT_LANES_GROUP 4
-#endif
-    constexpr int G = RT_LANES_GROUP;
+    constexpr int G = 4;
     auto rowidx = [&](int i) {
         const int r = 2 * (wave + kConeWaves * i) + h;
         return r < nrows ? r : nrows - 1;
@@ -1461,7 +1227,7 @@ __device__ __forceinline__ void store_rows_lanes(const float (&v)[RW][1], int p,
 }
 
 // kPack2 rows of p >= 8 bins as (row, 8-bin segment) tasks, one per lane
-// (RT_PACK_TASKS): task t = tid + kConeBlock * i is row t / segs, segment
+// (merge_step_tasks): task t = tid + kConeBlock * i is row t / segs, segment
 // t % segs, bins j0 .. j0 + 7 with j0 = min(8 * seg, p - 8) (the last
 // segment of a row overlaps the one before it when 8 does not divide p:
 // those bins are computed twice, identically, and written twice with the
@@ -1473,9 +1239,6 @@ __device__ __forceinline__ void store_rows_lanes(const float (&v)[RW][1], int p,
 // (same values, same addresses).  Levels above the fill at the odd stride
 // qs = p | 1 (the 32-lane halves of a read or write then hit distinct banks
 // for distinct rows).
-#ifndef RT_PACK_TASKS
-#define RT_PACK_TASKS 1
-#endif
 constexpr int kPackSeg = 8;
 constexpr int kPackTasks = 3;                 // tasks per lane: kMaxRows rows x 4 segments
 static_assert(kMaxRows * 4 <= kPackTasks * kConeBlock, "short-row tasks per lane");
@@ -1489,28 +1252,12 @@ __device__ __forceinline__ void pack_task(int t, int segs, int p, int& r, int& j
     j0 = min((t - r * segs) * kPackSeg, p - kPackSeg);
 }
 
-// x[e] = row[(j0 + s + e) mod p] of the row at LDS offset o (j0 + e < p, s < p)
-__device__ __forceinline__ void pack_rolled(lds_cptr sp, int o, int j0, int s, int p, float (&x)[kPackSeg])
-{
-    lds_cptr lo = sp + o + j0 + s;
-    lds_cptr hi = lo - p;
-    // opaque: one select of the two addresses per element (the element
-    // offset immediate), not a select of 0 / p folded into a shifted add
-    asm("" : "+v"(lo), "+v"(hi));
-    const int w = p - j0 - s;                 // first wrapped element
-#pragma unroll
-    for (int e = 0; e < kPackSeg; ++e) x[e] = lds_ld((e >= w ? hi : lo) + e);
-}
-
-// The same from the short-row roll table (RT_PACK_LUT): entry x = j0 + s
+// The same from the short-row roll table: entry x = j0 + s
 // (x < 2p <= 64) holds the byte offsets 4 ((x + e) mod p) of the segment's
 // eight elements as bytes: one conflict-free ds_read_b64 per rolled segment,
 // then one address add per element (byte select) instead of a compare and a
 // select.  Same LDS words: bit-exact.  The table lives in the metadata area,
 // which short-row units do not use (their blob is in their level buffer).
-#ifndef RT_PACK_LUT
-#define RT_PACK_LUT 1
-#endif
 __device__ __forceinline__ void pack_rolled_lut(lds_cptr sp, int o, unsigned long long e, float (&x)[kPackSeg])
 {
     const lds_ccptr rb = (lds_ccptr)(sp + o);
@@ -1568,21 +1315,13 @@ __device__ __forceinline__ void merge_step_tasks(const UnitCtx& C, const float* 
                 const int o3 = FIRST ? loff[q3] : (int)__umul24(q3, (uint32_t)qs);
                 float x2[kPackSeg], x3[kPackSeg];
                 const lds_cptr h0 = sp + o0 + j0;
-                if (RT_PACK_LUT) {
-                    // table entries first (plain loads), then the volatile reads
-                    const unsigned long long e1 = plut[j0 + sH], e2 = plut[j0 + sh], e3 = plut[j0 + sTT];
+                // table entries first (plain loads), then the volatile reads
+                const unsigned long long e1 = plut[j0 + sH], e2 = plut[j0 + sh], e3 = plut[j0 + sTT];
 #pragma unroll
-                    for (int k = 0; k < kPackSeg; ++k) x0[k] = lds_ld(h0 + k);
-                    pack_rolled_lut(sp, o1, e1, x1);
-                    pack_rolled_lut(sp, o2, e2, x2);
-                    pack_rolled_lut(sp, o3, e3, x3);
-                } else {
-#pragma unroll
-                    for (int k = 0; k < kPackSeg; ++k) x0[k] = lds_ld(h0 + k);
-                    pack_rolled(sp, o1, j0, sH, p, x1);
-                    pack_rolled(sp, o2, j0, sh, p, x2);
-                    pack_rolled(sp, o3, j0, sTT, p, x3);
-                }
+                for (int k = 0; k < kPackSeg; ++k) x0[k] = lds_ld(h0 + k);
+                pack_rolled_lut(sp, o1, e1, x1);
+                pack_rolled_lut(sp, o2, e2, x2);
+                pack_rolled_lut(sp, o3, e3, x3);
 #pragma unroll
                 for (int k = 0; k < kPackSeg; ++k) v[i][k] = __fadd_rn(__fadd_rn(x0[k], x1[k]), __fadd_rn(x2[k], x3[k]));
             } else {
@@ -1593,16 +1332,10 @@ __device__ __forceinline__ void merge_step_tasks(const UnitCtx& C, const float* 
                 const int ho = FIRST ? loff[d & 1023u] : (int)__umul24(d & 1023u, (uint32_t)qs);
                 const int to = car ? ho : (FIRST ? loff[tc & 1023u] : (int)__umul24(tc, (uint32_t)qs));
                 const lds_cptr h0 = sp + ho + j0;
-                if (RT_PACK_LUT) {
-                    const unsigned long long e1 = plut[j0 + (car ? 0 : sh)];
+                const unsigned long long e1 = plut[j0 + (car ? 0 : sh)];
 #pragma unroll
-                    for (int k = 0; k < kPackSeg; ++k) x0[k] = lds_ld(h0 + k);
-                    pack_rolled_lut(sp, to, e1, x1);
-                } else {
-#pragma unroll
-                    for (int k = 0; k < kPackSeg; ++k) x0[k] = lds_ld(h0 + k);
-                    pack_rolled(sp, to, j0, car ? 0 : sh, p, x1);
-                }
+                for (int k = 0; k < kPackSeg; ++k) x0[k] = lds_ld(h0 + k);
+                pack_rolled_lut(sp, to, e1, x1);
                 // a carried size-1 node adds -0.0 (x + (-0.0) == x: the reference's copy)
 #pragma unroll
                 for (int k = 0; k < kPackSeg; ++k) v[i][k] = __fadd_rn(x0[k], car ? -0.0f : x1[k]);
@@ -1616,9 +1349,6 @@ __device__ __forceinline__ void merge_step_tasks(const UnitCtx& C, const float* 
 // box, cone ms per cfg4 trial (profiles/r03zi_ab_cfg4.log): 0.771 / 0.772
 // with eight 4-byte stores per task, 0.679 / 0.679 with two 16-byte ones,
 // S/N identical.
-#ifndef RT_PACK_STORE16
-#define RT_PACK_STORE16 1
-#endif
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
 template <bool GLOBAL>
@@ -1635,19 +1365,13 @@ __device__ __forceinline__ void put_tasks(float* base, int q, const float (&v)[k
             pack_task(min(tid + kConeBlock * i, ntask - 1), segs, p, r, j0);
             if constexpr (GLOBAL) {
                 const uint32_t ob = st_o0 + (uint32_t)(r * p + j0) * 4u;
-                if constexpr (RT_PACK_STORE16) {
-                    // the task's 8 bins as two 16-byte stores (dword-aligned
-                    // multi-dword buffer stores)
+                // the task's 8 bins as two 16-byte stores (dword-aligned
+                // multi-dword buffer stores)
 #pragma unroll
-                    for (int k = 0; k < kPackSeg; k += 4) {
-                        const v4u w = {__float_as_uint(v[i][k]), __float_as_uint(v[i][k + 1]),
-                                       __float_as_uint(v[i][k + 2]), __float_as_uint(v[i][k + 3])};
-                        __builtin_amdgcn_raw_buffer_store_b128(w, rs, (int)(ob + 4u * k), 0, 0);
-                    }
-                } else {
-#pragma unroll
-                    for (int k = 0; k < kPackSeg; ++k)
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs, (int)(ob + 4u * k), 0, 0);
+                for (int k = 0; k < kPackSeg; k += 4) {
+                    const v4u w = {__float_as_uint(v[i][k]), __float_as_uint(v[i][k + 1]),
+                                   __float_as_uint(v[i][k + 2]), __float_as_uint(v[i][k + 3])};
+                    __builtin_amdgcn_raw_buffer_store_b128(w, rs, (int)(ob + 4u * k), 0, 0);
                 }
             } else {
                 float* const o = base + r * q + j0;
@@ -1667,7 +1391,7 @@ __device__ __forceinline__ void put_tasks(float* base, int q, const float (&v)[k
 template <int SMAX, int RW>
 __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int p, int L, int tid, bool st,
                                              __amdgpu_buffer_rsrc_t rs, uint32_t st_o0, uint32_t flags, float* dummy,
-                                             int qout, bool zpad)
+                                             int qout)
 {
     const int lane = tid & 63, wave = tid >> 6;
     const bool tile = C.tile;
@@ -1683,7 +1407,7 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
     // and for a last odd level
     const bool fuse = (flags & kConeFuse2) != 0;
     if constexpr (SMAX == kPack2) {
-        if (RT_PACK_TASKS && p >= kPackSeg) {
+        if (p >= kPackSeg) {
             const int qs = pack_stride(p);
             for (int l = L - 1; l >= 0;) {
                 const bool two = fuse && l >= 1 && (tile || (node_size >> l) >= 2);
@@ -1748,13 +1472,8 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
                 const int* lo_src = first ? loff : nullptr;
                 uint32_t sw;
                 int nq;
-                if (first || !RT_SLOT_FIRST) {
-                    if (two) merge_step_slots<SMAX, RW, true, true>(C, src, p, lo, lane, wave, v, lo_src, sw, nq);
-                    else merge_step_slots<SMAX, RW, false, true>(C, src, p, lo, lane, wave, v, lo_src, sw, nq);
-                } else {
-                    if (two) merge_step_slots<SMAX, RW, true, false>(C, src, p, lo, lane, wave, v, lo_src, sw, nq);
-                    else merge_step_slots<SMAX, RW, false, false>(C, src, p, lo, lane, wave, v, lo_src, sw, nq);
-                }
+                if (two) merge_step_slots<SMAX, RW, true>(C, src, p, lo, lane, wave, v, lo_src, sw, nq);
+                else merge_step_slots<SMAX, RW, false>(C, src, p, lo, lane, wave, v, lo_src, sw, nq);
                 l = lo - 1;
                 if (lo == 0 && st) {
                     store_rows_slots<SMAX, RW>(v, p, lane, sw, nq, rs, st_o0);
@@ -1763,8 +1482,7 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
                 if (!(flags & kConeDiagNoBarrier)) lds_barrier();
                 // the output level of a final pass at row stride qout (the S/N's)
                 if (!(flags & kConeDiagNoWrite))
-                    write_rows_slots<SMAX, RW>(base, dummy, v, p, lane, sw, nq, lo == 0 ? qout : p,
-                                               lo == 0 && zpad);
+                    write_rows_slots<SMAX, RW>(base, dummy, v, p, lane, sw, nq, lo == 0 ? qout : p);
                 if (!(flags & kConeDiagNoBarrier)) lds_barrier();
             }
             return;
@@ -1799,31 +1517,6 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
         }
         if (!(flags & kConeDiagNoBarrier)) lds_barrier();
     }
-}
-
-// Fused boxcar S/N (snr.hpp:37-65) of the output rows s < rows_eval held in LDS
-// (row stride p): G lanes per row, each lane a chunk of c <= CH columns held
-// in registers (c odd: the G chunks of a row start on distinct banks).
-// fp64 prefix: sequential in the chunk + log2(G)-step segmented scan
-// (kernels.hpp:73-86).  For G <= 16 (one DPP row) the scan, the per-width
-// max and the neighbour exchange run on DPP row shifts (VALU, no LDS
-// round trip); each lane then reads its window c[j0 .. j0 + CH + kSnrWin)
-// (the wrap c[p + j] = c[j] + sum applied once per element) and evaluates
-// every width w <= kSnrWin from registers.  Wider rows and wider widths use
-// the general path (shuffles, LDS reads per width).
-// (kSnrWin, kSnrMaxChunk: common.hpp)
-// rows per lane and S/N pass for 16-lane row groups (p = 129-272).  A/B
-// (ms per cfg2 trial): 2 rows (one pass per final unit instead of two,
-// independent chains interleaved) 9.13 vs 8.87 -- the doubled register
-// window spills ~37 SGPRs -- so 1.
-#ifndef RT_SNR_ROWS
-#define RT_SNR_ROWS 1
-#endif
-
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v)
-{
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 
 template <int CTRL>
@@ -1871,82 +1564,16 @@ __device__ __forceinline__ double seg_scan_dpp(double v, int lane)
     return v;
 }
 
-// row_shr:d keeping the lane's own value where the source is outside the
-// 16-lane row (bound_ctrl off, old = v)
-template <int CTRL>
-__device__ __forceinline__ float dpp_keep(float v)
-{
-    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-
-template <int CTRL, int ROWS>
-__device__ __forceinline__ float dpp_keep_rows(float v)
-{
-    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, ROWS, 0xF, false));
-}
-
-// max over the G lanes of a group, valid in lane g == G - 1.  fmaxf never
-// returns a NaN operand over a number, as diff_max's comparison.
-template <int G>
-__device__ __forceinline__ float seg_max_dpp(float v, int lane)
-{
-    if constexpr (G >= 16) {
-        v = fmaxf(v, dpp_keep<0x111>(v));
-        v = fmaxf(v, dpp_keep<0x112>(v));
-        v = fmaxf(v, dpp_keep<0x114>(v));
-        v = fmaxf(v, dpp_keep<0x118>(v));
-        if (G >= 32) v = fmaxf(v, dpp_keep_rows<0x142, 0xA>(v));
-        if (G >= 64) v = fmaxf(v, dpp_keep_rows<0x143, 0xC>(v));
-    } else {
-        const int g = lane & (G - 1);
-        float y = dpp_keep<0x111>(v);
-        v = g >= 1 ? fmaxf(v, y) : v;
-        y = dpp_keep<0x112>(v);
-        v = g >= 2 ? fmaxf(v, y) : v;
-        y = dpp_keep<0x114>(v);
-        v = g >= 4 ? fmaxf(v, y) : v;
-    }
-    return v;
-}
-
 // diff_max (kernels.hpp:50-60) of width W over the lane's columns (cp[i] =
-// +inf past the lane's chunk, so those differences are -inf)
-// A/B (ms per cfg2 trial): the window max as a v_max3 tree 8.82 vs the
-// dependent chain 8.78 -- the S/N is not bound by that chain; chain kept.
-#ifndef RT_SNR_TREE_MAX
-#define RT_SNR_TREE_MAX 0
-#endif
+// +inf past the lane's chunk, so those differences are -inf).
+// v_sub_f32 / v_max3_f32 as volatile asm: the width's work stays inside its
+// switch case (from plain code the compiler evaluated every case -- all
+// kSnrWin widths -- ahead of the width loop in every row pass).  v_max3_f32
+// (IEEE mode) never returns a quiet-NaN operand over a number, as diff_max's
+// comparison (kernels.hpp:50-60).
 template <int CH, int W>
 __device__ __forceinline__ float window_max(const float (&z)[CH + kSnrWin], const float (&cp)[CH])
 {
-#if RT_SNR_TREE_MAX
-    // the CH differences are independent; their max as a 3-ary tree
-    // (v_max3, depth log3 CH) instead of a CH-long dependent chain
-    float d[CH];
-#pragma unroll
-    for (int i = 0; i < CH; ++i) d[i] = __fsub_rn(z[i + W], cp[i]);
-    int n = CH;
-#pragma unroll
-    for (int step = 0; step < 4; ++step) {
-        if (n <= 1) break;
-#pragma unroll
-        for (int i = 0; i < (CH + 2) / 3; ++i) {
-            if (3 * i < n) {
-                const float a = d[3 * i];
-                const float b = 3 * i + 1 < n ? d[3 * i + 1] : -INFINITY;
-                const float c = 3 * i + 2 < n ? d[3 * i + 2] : -INFINITY;
-                d[i] = fmaxf(fmaxf(a, b), c);
-            }
-        }
-        n = (n + 2) / 3;
-    }
-    return d[0];
-#else
-    // v_sub_f32 / v_max3_f32 as volatile asm: the width's work stays inside
-    // its switch case (from plain code the compiler evaluated every case --
-    // all kSnrWin widths -- ahead of the width loop in every row pass).
-    // v_max3_f32 (IEEE mode) never returns a quiet-NaN operand over a
-    // number, as diff_max's comparison (kernels.hpp:50-60).
     float dm = -INFINITY;
 #pragma unroll
     for (int i = 0; i + 1 < CH; i += 2) {
@@ -1962,7 +1589,6 @@ __device__ __forceinline__ float window_max(const float (&z)[CH + kSnrWin], cons
                      : "v"(z[CH - 1 + W]), "v"(cp[CH - 1]));
     }
     return dm;
-#endif
 }
 
 // width dispatch: one switch (a jump, not a chain of scalar compares)
@@ -1987,44 +1613,6 @@ __device__ __forceinline__ float window_dispatch(int w, const float (&z)[CH + kS
     }
 }
 
-// the same for two rows at once (independent chains in one block)
-template <int CH, int W>
-__device__ __forceinline__ void window_max2(const float (&z0)[CH + kSnrWin], const float (&c0)[CH],
-                                            const float (&z1)[CH + kSnrWin], const float (&c1)[CH], float& d0,
-                                            float& d1)
-{
-    float m0 = -INFINITY, m1 = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < CH; ++i) {
-        m0 = fmaxf(m0, __fsub_rn(z0[i + W], c0[i]));
-        m1 = fmaxf(m1, __fsub_rn(z1[i + W], c1[i]));
-    }
-    d0 = m0;
-    d1 = m1;
-}
-
-template <int CH>
-__device__ __forceinline__ void window_dispatch2(int w, const float (&z0)[CH + kSnrWin], const float (&c0)[CH],
-                                                 const float (&z1)[CH + kSnrWin], const float (&c1)[CH], float& d0,
-                                                 float& d1)
-{
-    switch (w) {
-    case 1: window_max2<CH, 1>(z0, c0, z1, c1, d0, d1); break;
-    case 2: window_max2<CH, 2>(z0, c0, z1, c1, d0, d1); break;
-    case 3: window_max2<CH, 3>(z0, c0, z1, c1, d0, d1); break;
-    case 4: window_max2<CH, 4>(z0, c0, z1, c1, d0, d1); break;
-    case 5: window_max2<CH, 5>(z0, c0, z1, c1, d0, d1); break;
-    case 6: window_max2<CH, 6>(z0, c0, z1, c1, d0, d1); break;
-    case 7: window_max2<CH, 7>(z0, c0, z1, c1, d0, d1); break;
-    case 8: window_max2<CH, 8>(z0, c0, z1, c1, d0, d1); break;
-    case 9: window_max2<CH, 9>(z0, c0, z1, c1, d0, d1); break;
-    case 10: window_max2<CH, 10>(z0, c0, z1, c1, d0, d1); break;
-    case 11: window_max2<CH, 11>(z0, c0, z1, c1, d0, d1); break;
-    case 12: window_max2<CH, 12>(z0, c0, z1, c1, d0, d1); break;
-    default: d0 = d1 = -INFINITY; break;
-    }
-}
-
 // The standard ladder of small boxcar widths: generate_width_trials
 // (ffautils.py:3-10) with wtsp 1.5 always starts 1, 2, 3, 4, 6, 9 (every
 // BASELINE config: W = 6 or 10 from 240 bins).  When a plan's widths begin
@@ -2032,9 +1620,6 @@ __device__ __forceinline__ void window_dispatch2(int w, const float (&z0)[CH + k
 // (independent v_max3 chains the compiler may interleave, no width switch,
 // one interleaved DPP all-reduce), instead of one switch case and one
 // all-reduce per width.  Same float operations, same results.
-#ifndef RT_SNR_STD6
-#define RT_SNR_STD6 1
-#endif
 constexpr int kStdWidths[6] = {1, 2, 3, 4, 6, 9};
 
 template <int CH, int W>
@@ -2107,13 +1692,6 @@ __device__ __forceinline__ void snr_width_consts(int w, int p, float* out)
     out[1] = b;
 }
 
-// Transposed S/N emit (A/B knob; 0: the formula and a store per width in
-// every lane)
-#ifndef RT_SNR_TEMIT
-#define RT_SNR_TEMIT 1
-#endif
-constexpr bool kSnrTransEmit = RT_SNR_TEMIT != 0;
-
 // max over each G-lane group (G = 2 .. 64, groups aligned), in every lane
 // of the group: quad swaps, then the half-row and row mirrors, then (G >= 32)
 // cross-row exchanges (max never returns a NaN operand over a number, as
@@ -2139,36 +1717,24 @@ __device__ __forceinline__ float grp_allmax(float v)
     return v;
 }
 
-// Row passes without workgroup barriers: a row's lanes are one wave, so the
-// barrier per pass between the prefix writes and the window reads is not
-// needed for correctness.  A/B (ms per trial): on the round-2 mid S/N 9.10
-// vs 9.01 (slower); on the final S/N (transposed emit, no wrap selects)
-// cfg2 8.36 vs 8.43, cfg4 1.327 vs 1.34 -- on.
-#ifndef RT_SNR_WAVE_LOCAL
-#define RT_SNR_WAVE_LOCAL 1
-#endif
-// S/N prefix values as offset + the first pass's running sums (snr_rows).
-// A/B knob, off: neutral (cone ms per cfg2 trial 7.689 / 7.700 with it vs
-// 7.688 / 7.700, profiles/r03za_ab_*.log), and the second serial pass keeps
-// the reference's association of the row's additions after each lane's offset
-#ifndef RT_SNR_RUNSUM
-#define RT_SNR_RUNSUM 0
-#endif
-// S/N column masks from two wave-uniform lane masks (snr_rows col_ok).  A/B
-// knob, off: 17 fewer v_cmp per row pass, but cone ms per trial cfg2 7.76 vs
-// 7.68, cfg3 1.92 vs 1.91 with it (the SALU mask selects feed every column's
-// v_cndmask through VCC; profiles/r03v_ab_*.log)
-#ifndef RT_SNR_SMASK
-#define RT_SNR_SMASK 0
-#endif
-
-// NR rows per lane and pass (NR = 2: the lane's rows r and r + 512/G are
-// independent chains interleaved in one instruction stream, and half as many
-// row passes -- barriers, DPP scans -- per unit).
-template <int CH, int G, int NR = 1, bool WIDE = false>
+// Fused boxcar S/N (snr.hpp:37-65) of the output rows s < rows_eval held in
+// LDS (row stride q): G lanes per row, each lane a chunk of c <= CH columns
+// held in registers (c odd: the G chunks of a row start on distinct banks).
+// fp64 prefix: sequential in the chunk + log2(G)-step segmented scan
+// (kernels.hpp:73-86).  For G <= 16 (one DPP row) the scan and the width
+// maxima's all-reduce run on DPP row shifts (VALU, no LDS round trip); each
+// lane then reads its window c[j0 .. j0 + CH + kSnrWin) (the wrap c[p + j] =
+// c[j] + sum applied once per element) and evaluates every width w <= kSnrWin
+// from registers.  Wider widths read LDS per width.  Transposed emit: the
+// row's max of width iw goes to every lane of its group (DPP all-reduce) and
+// lane g keeps widths g, g + G, ...; one S/N formula (one fp32 division) and
+// one store per lane and slot after the widths, the stores of a row
+// consecutive.  Row passes without workgroup barriers: a row's G <= 64 lanes
+// are one wave, and a wave's LDS accesses complete in order.
+// (kSnrWin, kSnrMaxChunk: common.hpp)
+template <int CH, int G, bool WIDE = false>
 __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, float* data, int q, const int* wl,
-                                         int nev, int c, int tid, const float* whb, unsigned long long* tl,
-                                         bool zpad = false)
+                                         int nev, int c, int tid, const float* whb, unsigned long long* tl)
 {
     const int lane = tid & 63;
     const int p = U.p;
@@ -2188,27 +1754,11 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
     // conflict on every chunk and window read at p = 240-254)
     const bool natural = ext && wfull && (G - 1) * c + CH <= q;
     int j0 = natural ? g * c : min(g * c, p);
-    // every column a lane reads lies in [0, q), the merge cleared [p, q),
-    // and each lane's chunk is exactly its CH registers (c < CH: the columns
-    // past the chunk are the next lane's and stay masked)
-    const bool unmasked = zpad && natural && c == CH;
     int cnt = max(min(j0 + c, p) - j0, 0);        // columns of this lane (may be 0)
     const int owner = (p - 1) / c;
-    // Column masks as wave-uniform lane masks: a row's lanes hold c columns
-    // each except lane p / c, which holds p mod c (the later lanes none), so
-    // column i is valid in the lanes of m_any (i < p mod c), of m_full
-    // (p mod c <= i < c) or in none; the same for every row of the wave.  A
-    // column select is then one v_cndmask with an SGPR mask instead of a
-    // v_cmp against the lane's count and a v_cndmask.
-    const int cpart = uni(p % c);
-    const uint64_t m_any = __builtin_amdgcn_ballot_w64(cnt > 0);
-    const uint64_t m_full = __builtin_amdgcn_ballot_w64(cnt >= c);
-    auto col_ok = [&](int i) {
-        return __builtin_amdgcn_inverse_ballot_w64(i < cpart ? m_any : (i < c ? m_full : 0ull));
-    };
-    constexpr int kRowsPerSet = kConeBlock / G;
-    constexpr int rows_per_pass = NR * kRowsPerSet;
+    constexpr int rows_per_pass = kConeBlock / G;
     constexpr int writer = G - 1;
+    (void)writer;
     const uint32_t nw = a.num_widths;
     float* snr = a.snr + (uint64_t)U.trial * a.snr_stride + (U.snr_row + (uint64_t)U.s0) * (uint64_t)nw;
     const __amdgpu_buffer_rsrc_t srs = buffer_rsrc(snr, (uint32_t)nev * nw * 4u);
@@ -2224,91 +1774,33 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
         // recomputed by one v_cmp each instead of being hoisted out of the
         // loop into SGPR pairs that spill (two v_readlane per use)
         asm volatile("" : "+v"(j0), "+v"(cnt));
-        int r[NR];
-        bool active[NR];
-        float* row[NR];
-        float cp[NR][CH];
-        double part[NR];
-#pragma unroll
-        for (int k = 0; k < NR; ++k) {
-            r[k] = base + k * kRowsPerSet + (tid / G);
-            active[k] = r[k] < nev;
-            row[k] = data + min(r[k], nev - 1) * q + j0;
-        }
+        const int r = base + (tid / G);
+        const bool active = r < nev;
+        float* const row = data + min(r, nev - 1) * q + j0;
+        float cp[CH];
         // every lane reads CH columns at immediate offsets (past its chunk:
-        // the next chunk, the next row or the LDS pad), masked to 0 -- or,
-        // zero-padded rows (the merge stored +0.0 past p), unmasked
-        if (unmasked) {
+        // the next chunk, the next row or the LDS pad), masked to 0
 #pragma unroll
-            for (int k = 0; k < NR; ++k)
-#pragma unroll
-                for (int i = 0; i < CH; ++i) cp[k][i] = row[k][i];
-        } else {
-#pragma unroll
-            for (int k = 0; k < NR; ++k)
-#pragma unroll
-                for (int i = 0; i < CH; ++i) {
-                    const float x = row[k][i];
-                    cp[k][i] = (RT_SNR_SMASK ? col_ok(i) : i < cnt) ? x : 0.0f;
-                    // the select on the float, before the fp64 conversion (else
-                    // two selects on the converted halves)
-                    asm("" : "+v"(cp[k][i]));
-                }
+        for (int i = 0; i < CH; ++i) {
+            const float x = row[i];
+            cp[i] = i < cnt ? x : 0.0f;
+            // the select on the float, before the fp64 conversion (else two
+            // selects on the converted halves)
+            asm("" : "+v"(cp[i]));
         }
         // fp64 prefix: the masked columns add +0.0 (the partial sums start at
         // +0.0 and are never -0.0, so the additions are exact no-ops)
+        double part = 0.0;
 #pragma unroll
-        for (int k = 0; k < NR; ++k) part[k] = 0.0;
-#if RT_SNR_RUNSUM
-        // the lane's running sums kept from the first pass, so the prefix
-        // values are offset + run[i]: independent additions after the scan
-        // instead of a second serial chain of CH (the float64 sums of the
-        // row's floats are exact, as the lane-partial scan already assumes)
-        double run[NR][CH];
-#endif
+        for (int i = 0; i < CH; ++i) part = part + (double)cp[i];
+        double acc = dpp_d<0x138>(seg_scan_dpp<G>(part, lane));   // wave_shr:1 -- lane g takes lane g - 1
+        if (g == 0) acc = 0.0;
 #pragma unroll
-        for (int i = 0; i < CH; ++i)
-#pragma unroll
-            for (int k = 0; k < NR; ++k) {
-#ifdef RT_DIAG_SNR_F32
-                part[k] = (float)part[k] + cp[k][i];   // diagnostics only (wrong results)
-#else
-                part[k] = part[k] + (double)cp[k][i];
-#endif
-#if RT_SNR_RUNSUM
-                run[k][i] = part[k];
-#endif
-            }
-        double acc[NR];
-#pragma unroll
-        for (int k = 0; k < NR; ++k) {
-            const double incl = seg_scan_dpp<G>(part[k], lane);
-            acc[k] = dpp_d<0x138>(incl);              // wave_shr:1 -- lane g takes lane g - 1
-            if (g == 0) acc[k] = 0.0;
+        for (int i = 0; i < CH; ++i) {
+            acc = acc + (double)cp[i];
+            cp[i] = (float)acc;
         }
-#if RT_SNR_RUNSUM
-#pragma unroll
-        for (int i = 0; i < CH; ++i)
-#pragma unroll
-            for (int k = 0; k < NR; ++k) cp[k][i] = (float)(acc[k] + run[k][i]);
-#pragma unroll
-        for (int k = 0; k < NR; ++k) acc[k] = acc[k] + run[k][CH - 1];
-#else
-#pragma unroll
-        for (int i = 0; i < CH; ++i)
-#pragma unroll
-            for (int k = 0; k < NR; ++k) {
-#ifdef RT_DIAG_SNR_F32
-                acc[k] = (float)acc[k] + cp[k][i];   // diagnostics only (wrong results)
-#else
-                acc[k] = acc[k] + (double)cp[k][i];
-#endif
-                cp[k][i] = (float)acc[k];
-            }
-#endif
-        float sum[NR];
-#pragma unroll
-        for (int k = 0; k < NR; ++k) sum[k] = __shfl((float)acc[k], owner, G);
+        const float sum = __shfl((float)acc, owner, G);
         {
             // columns past the lane's chunk (and rows past nev) go to dummy
             // words in the LDS pad: a base select per column (the column an
@@ -2320,31 +1812,25 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
                 // lane's column i - c, which that lane writes later (a
                 // wave's LDS writes land in order), or lies past the row
                 // inside its stride (q >= p + CH)
+                if (active) {
+                    // volatile: the compiler keeps the descending order
+                    volatile __attribute__((address_space(3))) float* const rk =
+                        (volatile __attribute__((address_space(3))) float*)row;
 #pragma unroll
-                for (int k = 0; k < NR; ++k) {
-                    if (active[k]) {
-                        // volatile: the compiler keeps the descending order
-                        volatile __attribute__((address_space(3))) float* const rk =
-                            (volatile __attribute__((address_space(3))) float*)row[k];
-#pragma unroll
-                        for (int i = CH - 1; i >= 0; --i) rk[i] = cp[k][i];
-                    }
+                    for (int i = CH - 1; i >= 0; --i) rk[i] = cp[i];
                 }
             } else {
                 // one dummy word per lane and column (the same word for
                 // every lane serialised those stores on one bank)
                 const lds_ptr dummy = (lds_ptr)(data + kLdsDataFloats + 4 + lane);
+                int cw = active ? cnt : 0;
+                asm("" : "+v"(cw));
+                const lds_ptr rk = (lds_ptr)row;
 #pragma unroll
-                for (int k = 0; k < NR; ++k) {
-                    int cw = active[k] ? cnt : 0;
-                    asm("" : "+v"(cw));
-                    const lds_ptr rk = (lds_ptr)row[k];
-#pragma unroll
-                    for (int i = 0; i < CH; ++i) {
-                        lds_ptr b = i < cw ? rk : dummy;
-                        asm("" : "+v"(b));
-                        b[i] = cp[k][i];
-                    }
+                for (int i = 0; i < CH; ++i) {
+                    lds_ptr b = i < cw ? rk : dummy;
+                    asm("" : "+v"(b));
+                    b[i] = cp[i];
                 }
             }
         }
@@ -2353,213 +1839,143 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
         // stride) stored after the row by its own lanes (the wave's LDS
         // accesses complete in order), so the window reads below take
         // c[j0 .. j0 + CH + kSnrWin) -- and c[j0 + w ..] -- without a wrap
+        const float* const crow = data + min(r, nev - 1) * q;
         if (ext) {
-#pragma unroll
-            for (int k = 0; k < NR; ++k) {
-                float* const rb = data + min(r[k], nev - 1) * q;
-                auto put = [&](int e) {
-                    if (active[k] && e < next)
-                        *(volatile __attribute__((address_space(3))) float*)(rb + p + e) =
-                            __fadd_rn(lds_ld((lds_cptr)(rb + e)), sum[k]);
-                };
-                if constexpr (WIDE) {
-                    for (int e0 = 0; e0 < next; e0 += G) put(e0 + g);
-                } else {
-#pragma unroll
-                    for (int e0 = 0; e0 < kSnrWin; e0 += G) put(e0 + g);
-                }
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < NR; ++k)
-#pragma unroll
-            for (int i = 0; i < CH; ++i) cp[k][i] = (RT_SNR_SMASK ? col_ok(i) : i < cnt) ? cp[k][i] : INFINITY;
-        RT_SNR_MARK(7);
-#if RT_SNR_WAVE_LOCAL
-        // a row's G <= 64 lanes are one wave, and a wave's LDS accesses
-        // complete in order: its prefix writes are seen by its window reads
-        // below without a workgroup barrier (a compiler barrier only), so
-        // the waves of a unit run their row passes independently
-        __asm__ __volatile__("" ::: "memory");
-#else
-        lds_barrier();                        // prefix rows visible to all lanes
-#endif
-        RT_SNR_MARK(8);
-        const float* crow[NR];
-        uint32_t so[NR];
-#pragma unroll
-        for (int k = 0; k < NR; ++k) {
-            crow[k] = data + min(r[k], nev - 1) * q;
-            // one lane per row stores; the others store out of the buffer's
-            // range, which drops them (no exec-mask save/restore)
-            so[k] = (active[k] && g == writer) ? (uint32_t)r[k] * nw * 4u : 0x80000000u;
-        }
-        // transposed emit: the row's max of width iw goes to every
-        // lane of its group (DPP all-reduce) and lane g keeps widths g,
-        // g + G, ...; one S/N formula (one fp32 division) and one store per
-        // lane and slot after the widths, the stores of a row consecutive,
-        // instead of the formula and a store per width in every lane
-        constexpr bool TE = kSnrTransEmit;
-        constexpr int NSEL = TE ? (kMaxWidths + G - 1) / G : 1;
-        float sel[NR][NSEL] = {};
-        auto emit = [&](uint32_t iw, const float (&dmax)[NR]) {
-            if constexpr (TE) {
-#pragma unroll
-                for (int k = 0; k < NR; ++k) {
-                    const float dm = grp_allmax<G>(dmax[k]);
-#pragma unroll
-                    for (int sl = 0; sl < NSEL; ++sl)
-                        if (sl * G < (int)nw) sel[k][sl] = (int)iw == g + sl * G ? dm : sel[k][sl];
-                }
+            float* const rb = data + min(r, nev - 1) * q;
+            auto put = [&](int e) {
+                if (active && e < next)
+                    *(volatile __attribute__((address_space(3))) float*)(rb + p + e) =
+                        __fadd_rn(lds_ld((lds_cptr)(rb + e)), sum);
+            };
+            if constexpr (WIDE) {
+                for (int e0 = 0; e0 < next; e0 += G) put(e0 + g);
             } else {
-                // h + b and b of this width (per unit, in LDS: uniform reads)
-                const float hpb = __int_as_float(uni(__float_as_int(whb[2 * iw])));
-                const float b = __int_as_float(uni(__float_as_int(whb[2 * iw + 1])));
 #pragma unroll
-                for (int k = 0; k < NR; ++k) {
-                    const float dm = seg_max_dpp<G>(dmax[k], lane);
-                    const float v = (hpb * dm - b * sum[k]) / U.stdnoise;
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srs, (int)(so[k] + iw * 4u), 0, RT_SNR_CPOL);
-                }
+                for (int e0 = 0; e0 < kSnrWin; e0 += G) put(e0 + g);
             }
+        }
+#pragma unroll
+        for (int i = 0; i < CH; ++i) cp[i] = i < cnt ? cp[i] : INFINITY;
+        RT_SNR_MARK(7);
+        // a row's lanes are one wave: its prefix writes are seen by its
+        // window reads below without a workgroup barrier (a compiler barrier
+        // only), so the waves of a unit run their row passes independently
+        __asm__ __volatile__("" ::: "memory");
+        RT_SNR_MARK(8);
+        constexpr int NSEL = (kMaxWidths + G - 1) / G;
+        float sel[NSEL] = {};
+        auto emit = [&](uint32_t iw, float dmax) {
+            const float dm = grp_allmax<G>(dmax);
+#pragma unroll
+            for (int sl = 0; sl < NSEL; ++sl)
+                if (sl * G < (int)nw) sel[sl] = (int)iw == g + sl * G ? dm : sel[sl];
         };
         if constexpr (CH <= kSnrMaxChunk) {
             // widths <= kSnrWin from the register window c[j0 .. j0 + CH + kSnrWin)
-            float z[NR][CH + kSnrWin];
+            float z[CH + kSnrWin];
+            // two opaque bases (row and row - p), slot offsets immediate; one
+            // volatile read per element from the selected base (a plain read
+            // of each base was sunk into a branch per element, each with its
+            // own s_waitcnt lgkmcnt(0): 29 serialised LDS round trips per row
+            // pass)
+            lds_cptr za = (lds_cptr)(crow + j0);
+            lds_cptr zb = za - p;
+            asm("" : "+v"(za), "+v"(zb));
+            if (ext) {
+                // past the row: its wrapped extension (or, past that, words
+                // only differences with masked columns read)
 #pragma unroll
-            for (int k = 0; k < NR; ++k) {
-                // two opaque bases (row and row - p), slot offsets immediate;
-                // one volatile read per element from the selected base (a
-                // plain read of each base was sunk into a branch per element,
-                // each with its own s_waitcnt lgkmcnt(0): 29 serialised LDS
-                // round trips per row pass)
-                lds_cptr za = (lds_cptr)(crow[k] + j0);
-                lds_cptr zb = za - p;
-                asm("" : "+v"(za), "+v"(zb));
-                if (ext) {
-                    // past the row: its wrapped extension (or, past that,
-                    // words only differences with masked columns read)
+                for (int t = 0; t < CH + kSnrWin; ++t) z[t] = lds_ld(za + t);
+            } else {
+                // the wrap term as an addend (+0.0 before the wrap point: the
+                // prefix values are never -0.0, so x + 0.0 == x exactly), so
+                // no compare mask lives across the reads
+                float x[CH + kSnrWin], ad[CH + kSnrWin];
 #pragma unroll
-                    for (int t = 0; t < CH + kSnrWin; ++t) z[k][t] = lds_ld(za + t);
-                } else {
-                    // the wrap term as an addend (+0.0 before the wrap point:
-                    // the prefix values are never -0.0, so x + 0.0 == x
-                    // exactly), so no compare mask lives across the reads
-                    float x[CH + kSnrWin], ad[CH + kSnrWin];
-#pragma unroll
-                    for (int t = 0; t < CH + kSnrWin; ++t) {
-                        const bool wrap = j0 + t >= p;
-                        ad[t] = wrap ? sum[k] : 0.0f;
-                        x[t] = lds_ld((wrap ? zb : za) + t);
-                    }
-#pragma unroll
-                    for (int t = 0; t < CH + kSnrWin; ++t) z[k][t] = __fadd_rn(x[t], ad[t]);
+                for (int t = 0; t < CH + kSnrWin; ++t) {
+                    const bool wrap = j0 + t >= p;
+                    ad[t] = wrap ? sum : 0.0f;
+                    x[t] = lds_ld((wrap ? zb : za) + t);
                 }
+#pragma unroll
+                for (int t = 0; t < CH + kSnrWin; ++t) z[t] = __fadd_rn(x[t], ad[t]);
             }
             RT_SNR_MARK(9);
             uint32_t iw0 = 0;
-            if constexpr (RT_SNR_STD6 && NR == 1 && kSnrTransEmit && (G == 8 || G == 16)) {
+            if constexpr (G == 8 || G == 16) {
                 if (std6) {
                     // widths 0-5 are the standard ladder: lane g < 6 keeps width g
-                    sel[0][0] = snr_std6<CH, G>(z[0], cp[0], g);
+                    sel[0] = snr_std6<CH, G>(z, cp, g);
                     iw0 = 6;
                 }
             }
-#ifdef RT_DIAG_SNR_WIDTHS
-            for (uint32_t iw = iw0; iw < min(nw, (uint32_t)RT_DIAG_SNR_WIDTHS); ++iw) {   // diagnostics only (wrong results)
-#else
             for (uint32_t iw = iw0; iw < nw; ++iw) {
-#endif
                 const int w = __builtin_amdgcn_readlane(wlane, (int)iw);
-                if (w <= kSnrWin) {
-                    float dm[NR];
-#pragma unroll
-                    for (int k = 0; k < NR; ++k) dm[k] = -INFINITY;
-                    if constexpr (NR == 1) {
-                        dm[0] = window_dispatch<CH>(w, z[0], cp[0]);
-                    } else {
-                        window_dispatch2<CH>(w, z[0], cp[0], z[1], cp[1], dm[0], dm[1]);
-                    }
-                    emit(iw, dm);
-                }
+                if (w <= kSnrWin) emit(iw, window_dispatch<CH>(w, z, cp));
             }
         }
         // wider widths: the window c[j0 + w ..] read from LDS per width
         for (uint32_t iw = 0; iw < nw; ++iw) {
             const int w = __builtin_amdgcn_readlane(wlane, (int)iw);
             if (CH <= kSnrMaxChunk && w <= kSnrWin) continue;
-            float dmax[NR];
             if constexpr (CH <= kSnrMaxChunk) {
                 // c[j0 + w + t] for the lane's columns t at immediate offsets:
-                // WIDE, inside the row or its stored extension; else the
-                // wrap (j >= p) as a second base za - p and the addend sum
-                // (+0.0 before the wrap point: exact, the prefix values are
-                // never -0.0).  Columns past the chunk read words whose
-                // differences with cp = +inf are dropped.
+                // WIDE, inside the row or its stored extension; else the wrap
+                // (j >= p) as a second base za - p and the addend sum (+0.0
+                // before the wrap point: exact, the prefix values are never
+                // -0.0).  Columns past the chunk read words whose differences
+                // with cp = +inf are dropped.
+                lds_cptr za = (lds_cptr)(crow + j0 + w);
+                lds_cptr zb = za - p;
+                asm("" : "+v"(za), "+v"(zb));
+                float d[CH];
+                if constexpr (WIDE) {
 #pragma unroll
-                for (int k = 0; k < NR; ++k) {
-                    lds_cptr za = (lds_cptr)(crow[k] + j0 + w);
-                    lds_cptr zb = za - p;
-                    asm("" : "+v"(za), "+v"(zb));
-                    float d[CH];
-                    if constexpr (WIDE) {
+                    for (int t = 0; t < CH; ++t) d[t] = __fsub_rn(lds_ld(za + t), cp[t]);   // diff_max, kernels.hpp:50-60
+                } else {
+                    const int tw = p - j0 - w;        // first wrapped column
+                    float x[CH], ad[CH];
 #pragma unroll
-                        for (int t = 0; t < CH; ++t) d[t] = __fsub_rn(lds_ld(za + t), cp[k][t]);   // diff_max, kernels.hpp:50-60
-                    } else {
-                        const int tw = p - j0 - w;        // first wrapped column
-                        float x[CH], ad[CH];
-#pragma unroll
-                        for (int t = 0; t < CH; ++t) {
-                            const bool wrap = t >= tw;
-                            ad[t] = wrap ? sum[k] : 0.0f;
-                            x[t] = lds_ld((wrap ? zb : za) + t);
-                        }
-#pragma unroll
-                        for (int t = 0; t < CH; ++t) d[t] = __fsub_rn(__fadd_rn(x[t], ad[t]), cp[k][t]);
+                    for (int t = 0; t < CH; ++t) {
+                        const bool wrap = t >= tw;
+                        ad[t] = wrap ? sum : 0.0f;
+                        x[t] = lds_ld((wrap ? zb : za) + t);
                     }
-                    float m = d[0];
 #pragma unroll
-                    for (int t = 1; t + 1 < CH; t += 2) m = fmaxf(m, fmaxf(d[t], d[t + 1]));
-                    if constexpr (CH % 2 == 0) m = fmaxf(m, d[CH - 1]);
-                    dmax[k] = m;
+                    for (int t = 0; t < CH; ++t) d[t] = __fsub_rn(__fadd_rn(x[t], ad[t]), cp[t]);
                 }
-                emit(iw, dmax);
+                float m = d[0];
+#pragma unroll
+                for (int t = 1; t + 1 < CH; t += 2) m = fmaxf(m, fmaxf(d[t], d[t + 1]));
+                if constexpr (CH % 2 == 0) m = fmaxf(m, d[CH - 1]);
+                emit(iw, m);
                 continue;
             }
             const int last = max(cnt - 1, 0);
+            float dmax = -INFINITY;
+            float lv[CH];
 #pragma unroll
-            for (int k = 0; k < NR; ++k) {
-                dmax[k] = -INFINITY;
-                float lv[CH];
+            for (int t = 0; t < CH; ++t) {
+                const int j = j0 + min(t, last) + w;
+                lv[t] = crow[j >= p ? j - p : j];
+            }
 #pragma unroll
-                for (int t = 0; t < CH; ++t) {
-                    const int j = j0 + min(t, last) + w;
-                    lv[t] = crow[k][j >= p ? j - p : j];
-                }
-#pragma unroll
-                for (int i = 0; i < CH; ++i) {
-                    const bool wrap = j0 + min(i, last) + w >= p;
-                    const float ck = wrap ? __fadd_rn(lv[i], sum[k]) : lv[i];
-                    dmax[k] = fmaxf(dmax[k], __fsub_rn(ck, cp[k][i]));  // diff_max, kernels.hpp:50-60
-                }
+            for (int i = 0; i < CH; ++i) {
+                const bool wrap = j0 + min(i, last) + w >= p;
+                const float ck = wrap ? __fadd_rn(lv[i], sum) : lv[i];
+                dmax = fmaxf(dmax, __fsub_rn(ck, cp[i]));  // diff_max, kernels.hpp:50-60
             }
             emit(iw, dmax);
         }
-        if constexpr (TE) {
 #pragma unroll
-            for (int sl = 0; sl < NSEL; ++sl) {
-                if (sl * G < (int)nw) {
-                    const int iw = g + sl * G;
-                    const int iwc = min(iw, (int)nw - 1);
-                    const float hpb = whb[2 * iwc], b = whb[2 * iwc + 1];
-#pragma unroll
-                    for (int k = 0; k < NR; ++k) {
-                        const float v = (hpb * sel[k][sl] - b * sum[k]) / U.stdnoise;
-                        const uint32_t o = (active[k] && iw < (int)nw) ? ((uint32_t)r[k] * nw + (uint32_t)iw) * 4u
-                                                                       : 0x80000000u;
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srs, (int)o, 0, RT_SNR_CPOL);
-                    }
-                }
+        for (int sl = 0; sl < NSEL; ++sl) {
+            if (sl * G < (int)nw) {
+                const int iw = g + sl * G;
+                const int iwc = min(iw, (int)nw - 1);
+                const float hpb = whb[2 * iwc], b = whb[2 * iwc + 1];
+                const float v = (hpb * sel[sl] - b * sum) / U.stdnoise;
+                const uint32_t o = (active && iw < (int)nw) ? ((uint32_t)r * nw + (uint32_t)iw) * 4u : 0x80000000u;
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srs, (int)o, 0, kSnrCpol);
             }
         }
         RT_SNR_MARK(10);
@@ -2576,29 +1992,19 @@ constexpr bool variant_has_group(int smax, int G)
     return snr_group(variant_pmin(smax)) <= G && G <= snr_group(variant_pmax(smax));
 }
 
-// S/N lane-group size of the short-row variant (kPack2, p <= 32): 2, 4 or 8
-// lanes per row (8 = the general rule, snr_group).  A/B, same box, cone ms
-// per cfg4 trial (profiles/r03zf_ab_cfg4.log): G = 8 0.837 / 0.837, G = 4
-// 0.777 / 0.778, G = 2 0.796 / 0.797, S/N identical -- 4.
-#ifndef RT_SNR_SHORT_G
-#define RT_SNR_SHORT_G 4
-#endif
-constexpr int kSnrShortG = RT_SNR_SHORT_G;
-static_assert(kSnrShortG == 2 || kSnrShortG == 4 || kSnrShortG == 8, "RT_SNR_SHORT_G is 2, 4 or 8");
+// S/N lane-group size of the short-row variant (kPack2, p <= 32).  A/B, same
+// box, cone ms per cfg4 trial (profiles/r03zf_ab_cfg4.log): G = 8 0.837 /
+// 0.837, G = 4 0.777 / 0.778, G = 2 0.796 / 0.797, S/N identical -- 4.
+constexpr int kSnrShortG = 4;
 
 template <int SMAX, bool WIDE = false>
 __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& U, float* data, int q, const int* wl,
-                                             int nrows, int tid, float* whb, unsigned long long* tl, bool zpad = false)
+                                             int nrows, int tid, float* whb, unsigned long long* tl)
 {
     const int lane = tid & 63, wave = tid >> 6;
     const int p = U.p;
     const int nev = (int)min((int64_t)nrows, (int64_t)U.rows_eval - (int64_t)U.s0);
     if (nev <= 0) return;
-#if !RT_SNR_WAVE_LOCAL
-    // per-width constants of the S/N formula (snr.hpp:37-65), once per unit;
-    // visible to every wave after the first barrier of the row passes
-    if (tid < (int)a.num_widths) snr_width_consts(wl[tid], p, whb + 2 * tid);
-#endif
     // G lanes per row: the smallest power of two >= 8 whose chunks fit
     // kSnrMaxChunk columns; chunk lengths odd (the G chunks of a row start
     // on distinct banks)
@@ -2608,24 +2014,24 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
     if (c < kSnrMaxChunk) c |= 1;
     const uint32_t nw = a.num_widths;
     float* snr = a.snr + (uint64_t)U.trial * a.snr_stride + (U.snr_row + (uint64_t)U.s0) * (uint64_t)nw;
-    if constexpr (SMAX == kPack2 && kSnrShortG < 8) {
+    if constexpr (SMAX == kPack2) {
         // short rows (p <= 32): kSnrShortG lanes per row, so a pass covers
         // 512 / G rows (cfg4's ~380-row final units: 3 passes at G = 4
         // instead of 6 at G = 8)
         constexpr int GS = kSnrShortG;
         const int cs = ((p + GS - 1) / GS) | 1;
-        if (cs <= 5) snr_rows<5, GS>(a, U, data, q, wl, nev, cs, tid, whb, tl, zpad);
-        else if (cs <= 9) snr_rows<9, GS>(a, U, data, q, wl, nev, cs, tid, whb, tl, zpad);
-        else snr_rows<kSnrMaxChunk, GS>(a, U, data, q, wl, nev, cs, tid, whb, tl, zpad);
+        if (cs <= 5) snr_rows<5, GS>(a, U, data, q, wl, nev, cs, tid, whb, tl);
+        else if (cs <= 9) snr_rows<9, GS>(a, U, data, q, wl, nev, cs, tid, whb, tl);
+        else snr_rows<kSnrMaxChunk, GS>(a, U, data, q, wl, nev, cs, tid, whb, tl);
         return;
     }
     if (c <= kSnrMaxChunk) {
         // short rows (p <= 40 / 72): register chunks sized to the row, not 17
         if constexpr (variant_has_group(SMAX, 8)) {
             if (G == 8) {
-                if (c <= 5) snr_rows<5, 8>(a, U, data, q, wl, nev, c, tid, whb, tl, zpad);
-                else if (c <= 9) snr_rows<9, 8>(a, U, data, q, wl, nev, c, tid, whb, tl, zpad);
-                else snr_rows<kSnrMaxChunk, 8>(a, U, data, q, wl, nev, c, tid, whb, tl, zpad);
+                if (c <= 5) snr_rows<5, 8>(a, U, data, q, wl, nev, c, tid, whb, tl);
+                else if (c <= 9) snr_rows<9, 8>(a, U, data, q, wl, nev, c, tid, whb, tl);
+                else snr_rows<kSnrMaxChunk, 8>(a, U, data, q, wl, nev, c, tid, whb, tl);
                 return;
             }
         }
@@ -2633,23 +2039,23 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
             if (G == 16) {
                 if constexpr (WIDE) {
                     if (snr_wide_ok(p, q, wl[kMaxWidths])) {
-                        snr_rows<kSnrMaxChunk, 16, RT_SNR_ROWS, true>(a, U, data, q, wl, nev, c, tid, whb, tl, zpad);
+                        snr_rows<kSnrMaxChunk, 16, true>(a, U, data, q, wl, nev, c, tid, whb, tl);
                         return;
                     }
                 }
-                snr_rows<kSnrMaxChunk, 16, RT_SNR_ROWS>(a, U, data, q, wl, nev, c, tid, whb, tl, zpad);
+                snr_rows<kSnrMaxChunk, 16>(a, U, data, q, wl, nev, c, tid, whb, tl);
                 return;
             }
         }
         if constexpr (variant_has_group(SMAX, 32)) {
             if (G == 32) {
-                snr_rows<kSnrMaxChunk, 32>(a, U, data, q, wl, nev, c, tid, whb, tl, zpad);
+                snr_rows<kSnrMaxChunk, 32>(a, U, data, q, wl, nev, c, tid, whb, tl);
                 return;
             }
         }
-        if constexpr (variant_has_group(SMAX, 64)) snr_rows<kSnrMaxChunk, 64>(a, U, data, q, wl, nev, c, tid, whb, tl, zpad);
+        if constexpr (variant_has_group(SMAX, 64)) snr_rows<kSnrMaxChunk, 64>(a, U, data, q, wl, nev, c, tid, whb, tl);
     } else if (c <= kSnrChunk) {
-        if constexpr (variant_has_group(SMAX, 64)) snr_rows<kSnrChunk, 64>(a, U, data, q, wl, nev, c, tid, whb, tl, zpad);
+        if constexpr (variant_has_group(SMAX, 64)) snr_rows<kSnrChunk, 64>(a, U, data, q, wl, nev, c, tid, whb, tl);
     } else if constexpr (variant_pmax(SMAX) > 64 * kSnrChunk) {
         // very wide rows (p > 64 * kSnrChunk): one wave per row, chunks from LDS
         const int g = lane;
@@ -2711,60 +2117,26 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
 #endif
 
 // One kernel per merge slot width SMAX (units with ceil(p/64) <= SMAX), so each
-// gets its own register allocation.  Persistent: a workgroup takes units u =
-// blockIdx.x, blockIdx.x + gridDim.x, ... (unit u = item u / batch, trial u %
-// batch; items are sorted longest first).  One level buffer (kConeBuffers =
-// 1, two workgroups per CU): a unit's DMA is waited for at its start, the
-// CU's other workgroup filling the wait; two buffers (one workgroup per CU):
-// while unit u is merged in one, unit u + gridDim.x streams into the other.
+// gets its own register allocation; one workgroup per unit u = blockIdx.x
+// (unit u = item u / batch, trial u % batch; items are sorted longest first),
+// two workgroups per CU: a unit's DMA is waited for at its start, the CU's
+// other workgroup filling the wait.
 //   begin(u) [DMA] | wait | merge(u) | store or S/N(u)
-#ifndef RT_PRIO_HALF
-#define RT_PRIO_HALF 0
-#endif
 // WIDE: final units whose S/N takes the widths past its register window as
 // plain LDS windows (snr_wide_ok; a separate instantiation, so the plans
 // without such widths run code without it)
-// XCD-aware unit order: workgroups are dealt round-robin over the 8 XCDs
-// (blocks b and b + 8 share one, MI355X_MICROARCH.md "Workgroup dispatch"),
-// so with u = blockIdx.x the batch's trials of one item -- which read the
-// same unit record, blob and DMA segment table -- were spread over all 8
-// L2s.  Here the units of an item (u = item * batch + trial) go to one XCD:
-// XCD x takes items x, x + 8, ... in order, its blocks b = 8 i + x running
-// unit (8 (i / batch) + x) * batch + i % batch.  A bijection on the first
-// 8 * batch * floor(total / (8 * batch)) units, identity on the rest; the
-// global longest-first order is kept per XCD.  A/B knob, off: same box, cone
-// ms per trial cfg2 7.87 vs 7.79, cfg3 1.951 vs 1.924, cfg4 0.883 vs 0.871
-// with it (profiles/r03q_ab_*.log).
-#ifndef RT_XCD_MAP
-#define RT_XCD_MAP 0
-#endif
-__device__ __forceinline__ uint32_t xcd_unit(uint32_t b, uint32_t total, uint32_t batch)
-{
-    if (!RT_XCD_MAP || batch < 2) return b;
-    const uint32_t span = 8u * batch;
-    if (b >= total / span * span) return b;
-    const uint32_t i = b >> 3, x = b & 7u;
-    return ((i / batch) * 8u + x) * batch + i % batch;
-}
-
 template <int SMAX, int RWT = 0, bool WIDE = false>
 __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(ConeArgs a)
 {
     constexpr int RW = RWT ? RWT : merge_rows_per_wave(SMAX);   // register rows per wave
-    __shared__ __attribute__((aligned(16))) float data[kConeBuffers][kLdsBufFloats + kLdsPadFloats];
-    __shared__ __attribute__((aligned(16))) uint32_t aux[kConeBuffers][kAuxWords + kLutPad];   // the host blob (+ roll table)
+    __shared__ __attribute__((aligned(16))) float data[kLdsBufFloats + kLdsPadFloats];
+    __shared__ __attribute__((aligned(16))) uint32_t aux[kAuxWords + kLutPad];   // the host blob (+ roll table)
     // boxcar widths (LDS reads never wait on the S/N stores in flight), then
     // the widest of them
     __shared__ int wl[kMaxWidths + 1];
     __shared__ float whb[2 * kMaxWidths];   // S/N: h + b and b per width
 
     const int tid = threadIdx.x;
-#if RT_PRIO_HALF
-    // static priority for the second-dispatched half (waves 4-7, each
-    // sharing a SIMD with one of waves 0-3): MI355X_MICROARCH.md, two waves
-    // per SIMD, item 4
-    if (tid >= kConeBlock / 2) __builtin_amdgcn_s_setprio(1);
-#endif
 #ifdef RT_STAMPS
     const unsigned long long t_entry = __builtin_amdgcn_s_memtime();
     const unsigned long long r_entry = __builtin_amdgcn_s_memrealtime();
@@ -2772,7 +2144,7 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
 #endif
     const uint32_t total = a.num_items * a.batch;
     if (blockIdx.x >= total) return;
-    uint32_t u = kConeBuffers == 1 ? xcd_unit(blockIdx.x, total, a.batch) : blockIdx.x;
+    const uint32_t u = blockIdx.x;
     if (tid < (int)a.num_widths) wl[tid] = (int)a.widths[tid];   // visible after the first barrier
     if (tid == 0) {
         uint32_t wm = 0;
@@ -2780,186 +2152,132 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
         wl[kMaxWidths] = (int)wm;
     }
     const bool dma = !(a.flags & kConeDiagNoLand);
-    int b = 0;
     bool ok;
 #ifdef RT_STAMPS
-    UnitCtx C = unit_begin<SMAX, RW>(a, u, aux[0], data[0], tid, dma, ok, t_begin);
+    const UnitCtx C = unit_begin<SMAX, RW>(a, u, aux, data, tid, dma, ok, t_begin);
+    unsigned long long tl[kStampMarks] = {};
+    tl[0] = __builtin_amdgcn_s_memtime();
 #else
-    UnitCtx C = unit_begin<SMAX, RW>(a, u, aux[0], data[0], tid, dma, ok);
+    const UnitCtx C = unit_begin<SMAX, RW>(a, u, aux, data, tid, dma, ok);
 #endif
-    for (;;) {
-#ifdef RT_STAMPS
-        unsigned long long tl[kStampMarks] = {};
-        tl[0] = __builtin_amdgcn_s_memtime();
-#endif
-        const UnitView& U = C.U;
-        const int p = U.p;
-        const int L = U.levels;
-        float* const buf = data[b];
-#if RT_SNR_WAVE_LOCAL
-        // a final pass's per-width S/N constants, published by the barrier
-        // below (the S/N row passes have no barrier of their own)
-        if (U.dst == kSelSnr && tid < (int)a.num_widths) snr_width_consts(wl[tid], p, whb + 2 * tid);
-#endif
-        // the roll table of a 4-slot unit (past its blob's LDS part, which
-        // the DMA may still be writing), published by the barrier below
-        if constexpr (SMAX == 4 && RT_ROLL_LUT)
-            if (C.slots && ok) build_roll_lut4(aux[b] + kLut4Off, p, tid);
-        // the short-row roll table (RT_PACK_LUT) in the unused metadata area
-        if constexpr (SMAX == kPack2 && RT_PACK_LUT)
-            if (ok && p >= kPackSeg) build_pack_lut(aux[b], p, tid);
-        // every wave waits for its own DMA (the previous unit's stores count
-        // in the same in-order counter), the barrier publishes all of them
-        __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)
-        lds_barrier();
-        RT_MARK(1);
-        // one buffer: one unit per workgroup (a compile-time single pass, so
-        // nothing is hoisted out of a unit loop into long-lived registers)
-        const uint32_t un = u + gridDim.x;
-        const bool has_next = kConeBuffers == 2 && un < total;
-        bool ok_next = false;
-        UnitCtx Cn;
-        if (kConeBuffers == 2 && has_next) Cn = unit_begin<SMAX, RW>(a, un, aux[b ^ 1], data[b ^ 1], tid, dma, ok_next);
-        RT_MARK(2);
-        if (!ok) {
-            if (tid == 0 && a.error_flag) atomicOr(a.error_flag, 1);
-        } else {
-            // merge levels, deepest first; a non-final pass stores its output
-            // level straight from registers (st), a final pass keeps it in LDS
-            // for the S/N epilogue
-            const bool st = U.dst != kSelSnr;
-            const bool st_regs = st && (a.flags & kConeStoreFromRegs);
-            const float* dst = (U.dst == kSelPing ? a.ping : a.pong) + (uint64_t)U.trial * a.buf_stride + U.buf_off;
-            const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(dst, (((uint32_t)U.m * (uint32_t)p + 3u) & ~3u) * 4u);
-            const uint32_t o0 = (uint32_t)(U.node_start + U.s0) * (uint32_t)p * 4u;
-            const int n0 = rows_at(C, 0);
-            // a final pass's output level at a row stride = 16 (mod 32): the
-            // S/N epilogue's lane groups (two rows of 16 lanes per 32-lane LDS
-            // group, odd chunk strides) then read and write on distinct banks
-            // (at stride p they collided on up to 10 of 32 banks)
-            int qout = p;
-            // short rows in (row, segment) tasks: every level above the fill
-            // at the odd stride pack_stride(p)
-            if constexpr (SMAX == kPack2)
-                if (L > 0) qout = pack_stride(p);
-            if constexpr (SMAX <= 5 && SMAX != kPack2) {
-                // = 16 (mod 32) and >= p + kSnrMaxChunk (room for the S/N's
-                // whole-chunk prefix writes and its wrapped prefix
-                // extension), else >= p + kSnrWin (the extension only)
-                const int qa = p + kSnrMaxChunk + ((16 - ((p + kSnrMaxChunk) & 31)) & 31);
-                const int qb = p + kSnrWin + ((16 - ((p + kSnrWin) & 31)) & 31);
-                if (!st && L > 0 && C.slots && (a.flags & kConeFuse2) && (a.flags & kConeSnrStride)) {
-                    qout = n0 * qa <= kLdsDataFloats ? qa : (n0 * qb <= kLdsDataFloats ? qb : p);
-                    // widths past the register window: a stride with room for
-                    // their plain-LDS windows (snr_wide_stride), = 16 (mod 32)
-                    // where that fits too
-                    const int wmax = wl[kMaxWidths];
-                    if (WIDE && snr_group(p) == 16 && wmax > kSnrWin && wmax < p) {
-                        const int qw = snr_wide_stride(p, wmax);
-                        const int qwp = qw + ((16 - (qw & 31)) & 31);
-                        if (n0 * qwp <= kLdsDataFloats) qout = qwp;
-                        else if (n0 * qw <= kLdsDataFloats) qout = qw;
-                    }
+    const UnitView& U = C.U;
+    const int p = U.p;
+    const int L = U.levels;
+    float* const buf = data;
+    // a final pass's per-width S/N constants, published by the barrier below
+    // (the S/N row passes have no barrier of their own)
+    if (U.dst == kSelSnr && tid < (int)a.num_widths) snr_width_consts(wl[tid], p, whb + 2 * tid);
+    // the roll table of a 4-slot unit (past its blob's LDS part, which the
+    // DMA may still be writing), published by the barrier below
+    if constexpr (SMAX == 4)
+        if (C.slots && ok) build_roll_lut4(aux + kLut4Off, p, tid);
+    // the short-row roll table in the unused metadata area
+    if constexpr (SMAX == kPack2)
+        if (ok && p >= kPackSeg) build_pack_lut(aux, p, tid);
+    // every wave waits for its own DMA, the barrier publishes all of them
+    __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)
+    lds_barrier();
+    RT_MARK(1);
+    RT_MARK(2);
+    if (!ok) {
+        if (tid == 0 && a.error_flag) atomicOr(a.error_flag, 1);
+    } else {
+        // merge levels, deepest first; a non-final pass stores its output
+        // level straight from registers (st), a final pass keeps it in LDS
+        // for the S/N epilogue
+        const bool st = U.dst != kSelSnr;
+        const bool st_regs = st && (a.flags & kConeStoreFromRegs);
+        const float* dst = (U.dst == kSelPing ? a.ping : a.pong) + (uint64_t)U.trial * a.buf_stride + U.buf_off;
+        const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(dst, (((uint32_t)U.m * (uint32_t)p + 3u) & ~3u) * 4u);
+        const uint32_t o0 = (uint32_t)(U.node_start + U.s0) * (uint32_t)p * 4u;
+        const int n0 = rows_at(C, 0);
+        // a final pass's output level at a row stride = 16 (mod 32): the
+        // S/N epilogue's lane groups (two rows of 16 lanes per 32-lane LDS
+        // group, odd chunk strides) then read and write on distinct banks
+        // (at stride p they collided on up to 10 of 32 banks)
+        int qout = p;
+        // short rows in (row, segment) tasks: every level above the fill at
+        // the odd stride pack_stride(p)
+        if constexpr (SMAX == kPack2)
+            if (L > 0) qout = pack_stride(p);
+        if constexpr (SMAX <= 5 && SMAX != kPack2) {
+            // = 16 (mod 32) and >= p + kSnrMaxChunk (room for the S/N's whole-
+            // chunk prefix writes and its wrapped prefix extension), else >=
+            // p + kSnrWin (the extension only)
+            const int qa = p + kSnrMaxChunk + ((16 - ((p + kSnrMaxChunk) & 31)) & 31);
+            const int qb = p + kSnrWin + ((16 - ((p + kSnrWin) & 31)) & 31);
+            if (!st && L > 0 && C.slots && (a.flags & kConeFuse2) && (a.flags & kConeSnrStride)) {
+                qout = n0 * qa <= kLdsDataFloats ? qa : (n0 * qb <= kLdsDataFloats ? qb : p);
+                // widths past the register window: a stride with room for
+                // their plain-LDS windows (snr_wide_stride), = 16 (mod 32)
+                // where that fits too
+                const int wmax = wl[kMaxWidths];
+                if (WIDE && snr_group(p) == 16 && wmax > kSnrWin && wmax < p) {
+                    const int qw = snr_wide_stride(p, wmax);
+                    const int qwp = qw + ((16 - (qw & 31)) & 31);
+                    if (n0 * qwp <= kLdsDataFloats) qout = qwp;
+                    else if (n0 * qw <= kLdsDataFloats) qout = qw;
                 }
             }
-            // the S/N's chunks read without column masks (zero-padded rows):
-            // a final pass whose output level the row-slot write-back stores
-            // at the S/N stride with room for every lane's whole chunk
-            bool zpad = RT_SNR_ZPAD && !st && L > 0 && C.slots && (a.flags & kConeFuse2) &&
-                        SMAX <= 5 && SMAX != kPack2 && qout >= p + kSnrMaxChunk;
-            if (RT_SNR_ZPAD == 2) {
-                // zeros only from the last slot's lanes past p (stores they
-                // issue anyway): every lane up to the row's owner must read
-                // its whole chunk inside the slots, [p, 64 SMAX), and those
-                // bins must lie inside the row stride
-                int G = 8;
-                while (G < 64 && (((p + G - 1) / G) | 1) > kSnrMaxChunk) G <<= 1;
-                int c = (p + G - 1) / G;
-                if (c < kSnrMaxChunk) c |= 1;
-                zpad = zpad && ((p - 1) / c + 1) * c <= 64 * SMAX && qout >= 64 * SMAX;
-            }
-            if (L > 0 && !(a.flags & kConeDiagNoMerge))
-                merge_levels<SMAX, RW>(C, buf, p, L, tid, st_regs, rs, o0, a.flags, buf + kLdsBufFloats + 4 + (tid & 63),
-                                       qout, zpad);
-            RT_MARK(3);
-            // the output level: dense rows from the buffer start, or (no merge
-            // level) the single bottom row where the DMA left it
-            float* const obase = L > 0 ? buf : buf + (C.table ? uni(bottom_offsets(C)[0]) : C.al);
-            if (st) {
-                if (L == 0 || !st_regs) {
-                    const int qst = L > 0 ? qout : p;    // the merged level's LDS row stride
-                    for (int r = 0; r < n0; ++r)
-                        for (int j = tid; j < p; j += kConeBlock)
-                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(obase[r * qst + j]), rs,
-                                                                  (int)(o0 + (uint32_t)(r * p + j) * 4u), 0, RT_STORE_CPOL);
-                }
-            } else {
-#ifdef RT_STAMPS
-                if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(a, U, obase, qout, wl, n0, tid, whb, tl, zpad);
-#else
-                if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(a, U, obase, qout, wl, n0, tid, whb, nullptr, zpad);
-#endif
-            }
         }
-        lds_barrier();                        // the level buffer is free
-#ifdef RT_STAMPS
-        RT_MARK(4);
-        tl[5] = t_entry;
-        tl[11] = t_begin[0];
-        tl[12] = t_begin[1];
-        tl[13] = t_begin[2];
-        if (kConeBuffers == 1 && (a.flags & kConeDiagExitWait)) __builtin_amdgcn_s_waitcnt(0x0F70);
-        RT_MARK(6);
-        tl[14] = r_entry;
-        tl[15] = __builtin_amdgcn_s_memrealtime();
-        if (tid == 0 && a.stamps) {
-            unsigned long long* e = a.stamps + (uint64_t)kStampRecWords * (uint64_t)u;
-            const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));     // HW_REG_HW_ID
-            const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11));   // HW_REG_XCC_ID
-            e[0] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
-#pragma unroll
-            for (int i = 0; i < kStampMarks; ++i) e[1 + i] = tl[i];
-            e[1 + kStampMarks] = (unsigned long long)p | ((unsigned long long)L << 16) |
-                                 ((unsigned long long)U.mode << 24) | ((unsigned long long)rows_at(C, 0) << 32) |
-                                 ((unsigned long long)(U.dst == kSelSnr) << 48);
-        }
-#endif
-        if (!has_next) break;
-        u = un;
-        if (kConeBuffers == 2) {
-            b ^= 1;
-            C = Cn;
-            ok = ok_next;
+        if (L > 0 && !(a.flags & kConeDiagNoMerge))
+            merge_levels<SMAX, RW>(C, buf, p, L, tid, st_regs, rs, o0, a.flags, buf + kLdsBufFloats + 4 + (tid & 63),
+                                   qout);
+        RT_MARK(3);
+        // the output level: dense rows from the buffer start, or (no merge
+        // level) the single bottom row where the DMA left it
+        float* const obase = L > 0 ? buf : buf + (C.table ? uni(bottom_offsets(C)[0]) : C.al);
+        if (st) {
+            if (L == 0 || !st_regs) {
+                const int qst = L > 0 ? qout : p;    // the merged level's LDS row stride
+                for (int r = 0; r < n0; ++r)
+                    for (int j = tid; j < p; j += kConeBlock)
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(obase[r * qst + j]), rs,
+                                                              (int)(o0 + (uint32_t)(r * p + j) * 4u), 0, kStoreCpol);
+            }
         } else {
-            C = unit_begin<SMAX, RW>(a, u, aux[0], data[0], tid, dma, ok);
+#ifdef RT_STAMPS
+            if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(a, U, obase, qout, wl, n0, tid, whb, tl);
+#else
+            if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(a, U, obase, qout, wl, n0, tid, whb, nullptr);
+#endif
         }
     }
-    // two buffers: no DMA outstanding at exit (LDS DMA into a freed
-    // allocation); one buffer: every DMA was waited for at the unit start,
-    // and the unit's global stores need no wait before the end of the program
-    if (kConeBuffers == 2 || (a.flags & kConeDiagExitWait)) __builtin_amdgcn_s_waitcnt(0x0F70);
+#ifdef RT_STAMPS
+    lds_barrier();
+    RT_MARK(4);
+    tl[5] = t_entry;
+    tl[11] = t_begin[0];
+    tl[12] = t_begin[1];
+    tl[13] = t_begin[2];
+    RT_MARK(6);
+    tl[14] = r_entry;
+    tl[15] = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0 && a.stamps) {
+        unsigned long long* e = a.stamps + (uint64_t)kStampRecWords * (uint64_t)u;
+        const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));     // HW_REG_HW_ID
+        const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11));   // HW_REG_XCC_ID
+        e[0] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+#pragma unroll
+        for (int i = 0; i < kStampMarks; ++i) e[1 + i] = tl[i];
+        e[1 + kStampMarks] = (unsigned long long)p | ((unsigned long long)L << 16) |
+                             ((unsigned long long)U.mode << 24) | ((unsigned long long)rows_at(C, 0) << 32) |
+                             ((unsigned long long)(U.dst == kSelSnr) << 48);
+    }
+#endif
+    // every DMA was waited for at the unit start, and the unit's global
+    // stores need no wait before the end of the program
 }
 
-// Persistent grid: kConeWgsPerCu workgroups per CU (RIPTIDE_AMD_CONE_PERSIST=0:
-// one workgroup per unit, for A/B).
+// One workgroup per unit: the hardware dispatcher keeps both of a CU's
+// workgroup slots busy to the end of the launch (measured: 10.37 vs 11.55 ms
+// per cfg2 trial against a persistent grid, round 1).
 hipError_t launch_cone(const ConeArgs& args, uint32_t smax, uint32_t rw, bool wide_snr, hipStream_t s)
 {
     if (!args.num_items || !args.batch) return hipSuccess;
     const uint64_t total = (uint64_t)args.num_items * args.batch;
     if (total > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    uint64_t grid = (uint64_t)cus * kConeWgsPerCu;
-    // persistent workgroups only with two level buffers (their point is the
-    // prefetch; RIPTIDE_AMD_CONE_PERSIST=0 turns them off); with one buffer a
-    // workgroup per unit keeps both of a CU's workgroup slots busy to the end
-    // of the launch (measured: 10.37 vs 11.55 ms per cfg2 trial persistent).
-    static const bool persist = [] {
-        const char* e = std::getenv("RIPTIDE_AMD_CONE_PERSIST");
-        return kConeBuffers == 2 && (e ? std::atoi(e) != 0 : true);
-    }();
-    if (!persist || grid > total) grid = total;
-    const dim3 g((uint32_t)grid), b(kConeBlock);
+    const dim3 g((uint32_t)total), b(kConeBlock);
     switch (smax) {
     case 1:
         switch (rw) {

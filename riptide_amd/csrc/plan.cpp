@@ -291,7 +291,7 @@ static double item_cost(const ConeItem& it, const FfaXform& X)
 // path).  RIPTIDE_AMD_SNR_WIDE=0 drops the cap (A/B).
 static bool wide_snr(const FfaXform& X, int smax, bool snr_epilogue, uint32_t max_width)
 {
-    if (!RT_SNR_WIDE_EXT || !snr_epilogue || smax > 5 || smax == kPack2) return false;
+    if (!snr_epilogue || smax > 5 || smax == kPack2) return false;
     if (snr_group((int)X.p) != 16 || (int)max_width <= kSnrWin || max_width >= X.p) return false;
     if (const char* e = std::getenv("RIPTIDE_AMD_SNR_WIDE"))
         if (e[0] == '0') return false;
@@ -455,7 +455,7 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
 
 // Row slots of one merge step (output level with n rows, descriptors d):
 // rows in order, a pair where rows r, r + 1 share head and tail rows with
-// shifts s, s + 1 (never carried rows), else (RT_SLOT_HALF) a half where
+// shifts s, s + 1 (never carried rows), else a half where
 // they share only the head row (neither carried), filled into the slots
 // g = wave + 8q of the wave's register rows 2q, 2q + 1 (capacity 2, or 1 for
 // the last slot of an odd RW).  Every slot is filled to its capacity (a pair
@@ -470,7 +470,7 @@ static void build_row_slots(const uint32_t* d, uint32_t n, uint32_t p, int rw, s
         if (r + 1 < n && ((a ^ d[r + 1]) & 0xFFFFFu) == 0 && !carried && (d[r + 1] >> 20) == ((a >> 20) + 1) % p) {
             items.push_back({r, kSlotPair});
             r += 2;
-        } else if (RT_SLOT_HALF && r + 1 < n && ((a ^ d[r + 1]) & 1023u) == 0 && !carried &&
+        } else if (r + 1 < n && ((a ^ d[r + 1]) & 1023u) == 0 && !carried &&
                    ((d[r + 1] >> 10) & 1023u) != kCarriedRow) {
             items.push_back({r, kSlotHalf});
             r += 2;
@@ -773,6 +773,21 @@ void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, int smax, std:
     std::copy(segs.begin(), segs.end(), w + runoff);
 }
 
+// The 4-slot roll table sits at kLut4Off, past every 4-slot unit's blob LDS
+// part.  Worst case of that part: the header, <= 72 bottom-row offsets (the
+// 4-slot capacity: 8 waves x kRw4 register rows), 16-byte alignment, and the
+// resolved slot tables of <= 4 merge steps (whole units have <= 7 levels, of
+// which only the deepest can hold size-1 nodes: 1 + ceil(6 / 2) steps; tiles
+// <= kMaxTileLevels = 6 fused levels: 3 steps), each 4 header words + two
+// 16-byte entries per slot of every wave.  So a tile never needs to shrink
+// for the table, and validate_blob's check below can only fire on a broken
+// build.
+constexpr int kMaxSteps4 = 4;
+constexpr int kBlobLds4Worst =
+    kBlobHeader + kConeWaves * kRw4 + 3 + kMaxSteps4 * (4 + 4 * 2 * kConeWaves * ((kRw4 + 1) / 2));
+static_assert(kBlobLds4Worst <= kLut4Off, "4-slot unit blobs may overlap the roll table");
+static_assert((kMaxTileLevels + 1) / 2 <= kMaxSteps4, "tile steps");
+
 // A unit's blob as the kernel will read it: the DMA segments tile the fill
 // [0, fill chunks) in order, each <= 64 chunks inside the level buffer; every
 // row-slot table covers its step's output rows exactly once, a pair's rows
@@ -787,7 +802,7 @@ static void validate_blob(const ConeItem& it, uint32_t p, int smax, int rw, cons
         throw std::runtime_error("schedule: malformed unit blob header");
     if (4 * fill > (uint32_t)kLdsBufFloats) throw std::runtime_error("schedule: unit fill exceeds the LDS level buffer");
     // a 4-slot row-slot unit's roll table follows its blob's LDS part
-    if (RT_ROLL_LUT && smax == 4 && slot_words && runoff > (uint32_t)kLut4Off)
+    if (smax == 4 && slot_words && runoff > (uint32_t)kLut4Off)
         throw std::runtime_error("schedule: unit blob overlaps the roll table");
     uint32_t c = 0;
     const uint32_t K = (nseg + kConeWaves - 1) / kConeWaves;   // wave-major segment order

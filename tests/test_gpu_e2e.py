@@ -19,6 +19,7 @@ import hashlib
 import json
 import os
 import socket
+import sys
 import threading
 
 import numpy as np
@@ -298,30 +299,52 @@ def test_worker_pool_mixed_shapes_matches_per_file(e2e, tmp_path):
 
 
 # ---------------------------------------------------------------- C ABI robustness
+_ERROR_FLAG_BODY = r"""
+import sys
+import numpy as np
+import pytest
+import torch
+sys.path[:0] = [REPO, GOLDEN]
+import inputs
+from riptide_amd import _lib, engine, libcpp
+assert _lib.LIB_PATH.endswith("libriptide_amd_testhooks.so")
+case = inputs.PGRAM_CASES[1]
+x = torch.from_numpy(inputs.pgram_input(case)).cuda()
+args = (case["n"], case["tsamp"], case["pmin"], case["pmax"], case["bmin"], case["bmax"])
+good = engine.PeriodogramPlan.for_search(*args, ducy_max=case["ducy_max"])
+good.run(x, check=True)                                # no error on a valid plan
+lib = _lib.load()
+lib.rt_test_corrupt_next_plans(1)                      # test-only C entry point
+try:
+    bad = engine.PeriodogramPlan.for_search(*args, ducy_max=case["ducy_max"])
+    with pytest.raises(_lib.EngineError, match="LDS budget"):
+        bad.run(x, check=True)
+    bad.check()                                       # the flag was cleared by the failed check
+    with pytest.raises(_lib.EngineError, match="LDS budget"):
+        libcpp.periodogram(inputs.pgram_input(case), case["tsamp"], good.widths, case["pmin"], case["pmax"],
+                           case["bmin"], case["bmax"])
+finally:
+    lib.rt_test_corrupt_next_plans(0)
+good.check()
+print("error-flag OK")
+"""
+
+
 def test_plan_device_error_flag():
     """A unit that breaks its budget is refused by the kernel, which raises
     the plan's sticky flag; PeriodogramPlan.check / run(check=True) and the
-    host-buffer periodogram raise instead of returning unwritten rows."""
-    import torch
-    from riptide_amd import _lib, engine, libcpp
-    case = inputs.PGRAM_CASES[1]
-    x = torch.from_numpy(inputs.pgram_input(case)).cuda()
-    args = (case["n"], case["tsamp"], case["pmin"], case["pmax"], case["bmin"], case["bmax"])
-    good = engine.PeriodogramPlan.for_search(*args, ducy_max=case["ducy_max"])
-    good.run(x, check=True)                                # no error on a valid plan
-    lib = _lib.load()
-    lib.rt_test_corrupt_next_plans(1)                      # test-only C entry point
-    try:
-        bad = engine.PeriodogramPlan.for_search(*args, ducy_max=case["ducy_max"])
-        with pytest.raises(_lib.EngineError, match="LDS budget"):
-            bad.run(x, check=True)
-        bad.check()                                       # the flag was cleared by the failed check
-        with pytest.raises(_lib.EngineError, match="LDS budget"):
-            libcpp.periodogram(inputs.pgram_input(case), case["tsamp"], good.widths, case["pmin"], case["pmax"],
-                               case["bmin"], case["bmax"])
-    finally:
-        lib.rt_test_corrupt_next_plans(0)
-    good.check()
+    host-buffer periodogram raise instead of returning unwritten rows.  The
+    corrupting hook exists only in the test build of the library
+    (libriptide_amd_testhooks.so), so the body runs in a child process that
+    loads that build (RIPTIDE_AMD_LIB)."""
+    import subprocess
+    from riptide_amd import _lib
+    assert os.path.exists(_lib.TESTHOOKS_PATH), "build the test library: make -C riptide_amd/csrc"
+    env = dict(os.environ, RIPTIDE_AMD_LIB=_lib.TESTHOOKS_PATH)
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = f"REPO = {repo!r}\nGOLDEN = {os.path.join(repo, 'tests', 'golden')!r}\n" + _ERROR_FLAG_BODY
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "error-flag OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
 
 
 def test_two_host_threads_one_device():

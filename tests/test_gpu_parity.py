@@ -360,6 +360,11 @@ def test_full_config(rt, golden_full, name):
     d = torch.from_numpy(raw).cuda()
     x = engine.deredden_normalise(d, int(round(4.0 / c["tsamp"])), 101)
     snrs = plan.run(x).cpu().numpy()
+    _check_full_snrs(rt, g, c, plan, periods, foldbins, snrs)
+
+
+def _check_full_snrs(rt, g, c, plan, periods, foldbins, snrs):
+    """The golden_full checks of one full-size configuration's S/N."""
     # >= 5000 sampled rows, including the first and last evaluated row of
     # every FFA transform (tile / pass boundaries of the cone schedule)
     rows = np.asarray(g["sample_rows"])
@@ -378,6 +383,37 @@ def test_full_config(rt, golden_full, name):
     peaks, _ = rt.find_peaks(pg)
     got = [[p.ip, p.iw] for p in peaks]
     assert got == [[p[0], p[1]] for p in g["peaks"]]     # identical candidate list
+
+
+def test_bench_schedule_cfg2(rt, golden_full, monkeypatch):
+    """The schedule bench.py times: the whole cfg2 plan
+    in ONE transform group (RIPTIDE_AMD_SCRATCH_MFLOATS=1536: 14 cone
+    launches, every transform's scratch side by side) at batch 2, against the
+    golden cfg2 results (trial 0: the golden input) and bit-identical to the
+    default 96 Mi-float grouping (both trials; trial 1 the golden input
+    reversed, so the batch's trials differ)."""
+    import torch
+    from riptide_amd import engine
+    g = golden_full["configs"]["cfg2"]
+    c = g["case"]
+    raw = inputs.full_input(c)
+    if sha(raw) != g["input_sha"]:
+        pytest.fail(f"input generator drifted on this host: input sha256 {sha(raw)} != golden {g['input_sha']}")
+    args = (c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"])
+    monkeypatch.setenv("RIPTIDE_AMD_SCRATCH_MFLOATS", "1536")
+    one = engine.PeriodogramPlan.for_search(*args, ducy_max=c["ducy_max"])
+    monkeypatch.delenv("RIPTIDE_AMD_SCRATCH_MFLOATS")
+    dflt = engine.PeriodogramPlan.for_search(*args, ducy_max=c["ducy_max"])
+    s1, s0 = one.stats(), dflt.stats()
+    assert s1["launches"] <= 16 < s0["launches"], (s1, s0)     # one group vs many
+    d = torch.from_numpy(np.stack([raw, raw[::-1].copy()])).cuda()
+    x = engine.deredden_normalise(d, int(round(4.0 / c["tsamp"])), 101)
+    got = one.run(x, check=True)
+    ref = dflt.run(x, check=True)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref), "one-group schedule differs from the default grouping"
+    periods, foldbins = one.grid()
+    _check_full_snrs(rt, g, c, one, periods, foldbins, got[0].cpu().numpy())
 
 
 # ---------------------------------------------------------------- device peak detection (SURVEY.md §8 f1)

@@ -39,6 +39,41 @@ def test_header_symbols_exported(lib):
     assert set(_lib.EXPORTED) <= declared
 
 
+def test_test_hooks_only_in_test_build(lib):
+    """The fault-injection entry point is not part of the product library;
+    the test build (libriptide_amd_testhooks.so) carries it."""
+    import ctypes as ct
+    from riptide_amd import _lib
+    assert not hasattr(lib, "rt_test_corrupt_next_plans")
+    assert "rt_test_corrupt_next_plans" not in _lib.EXPORTED
+    t = ct.CDLL(_lib.TESTHOOKS_PATH, mode=ct.RTLD_LOCAL)
+    assert hasattr(t, "rt_test_corrupt_next_plans")
+    text = open(os.path.join(os.path.dirname(HEADER), "riptide_amd_test.h")).read()
+    assert "int rt_test_corrupt_next_plans(int on);" in text
+
+
+def _ladder(lib, n, c):
+    fused = ctypes.c_int(-1)
+    rungs = ctypes.c_uint64()
+    rc = lib.rt_ladder_check(n, c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"], ctypes.byref(fused),
+                             ctypes.byref(rungs))
+    assert rc == 0, lib.rt_last_error()
+    return fused.value, rungs.value
+
+
+def test_ladder_path_choice(lib):
+    """The fused ladder indexes samples in 32 bits: series of 2^29 samples or
+    more take the per-rung (64-bit) kernel (the planner enforces
+    the fused kernel's index range instead of assuming it)."""
+    c = dict(tsamp=256e-6, pmin=0.1, pmax=10.0, bmin=240, bmax=260)
+    assert _ladder(lib, 1 << 23, c)[0] == 1            # cfg2: fused
+    assert _ladder(lib, (1 << 29) - 1, c)[0] == 1
+    assert _ladder(lib, 1 << 29, c)[0] == 0            # 2^29: per-rung
+    assert _ladder(lib, (1 << 30) + 7, c)[0] == 0
+    f, r = _ladder(lib, 1 << 23, c)
+    assert r > 0
+
+
 def test_version(lib):
     assert b"gfx950" in lib.rt_version()
 
@@ -221,3 +256,65 @@ def test_ffa_schedules_validate(lib):
         assert lib.rt_ffa_schedule_check(m, p, ctypes.byref(n)) == 0, (m, p, lib.rt_last_error())
         assert n.value >= 1
     assert lib.rt_ffa_schedule_check(0, 16, None) == 1
+
+
+# ---------------------------------------------------------------- host sanitizers
+def _asan_cases():
+    from riptide_amd.ffautils import generate_width_trials
+    cases = []
+    for c in inputs.FULL_CASES:
+        w = len(generate_width_trials(c["bmin"], ducy_max=c["ducy_max"], wtsp=1.5))
+        cases.append((c["name"], ["pgram", c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"], w], {}))
+    c2 = inputs.FULL_CASES[1]
+    w2 = len(generate_width_trials(c2["bmin"], ducy_max=c2["ducy_max"], wtsp=1.5))
+    cases.append(("cfg2-bench-1536M", ["pgram", c2["n"], c2["tsamp"], c2["pmin"], c2["pmax"], c2["bmin"], c2["bmax"], w2],
+                  {"RIPTIDE_AMD_SCRATCH_MFLOATS": "1536"}))
+    c5 = inputs.CFG5
+    for r in c5["ranges"]:
+        f = r["ffa_search"]
+        w = len(generate_width_trials(f["bins_min"], ducy_max=0.2, wtsp=f["wtsp"]))
+        cases.append((f"cfg5-{r['name']}", ["pgram", c5["n"], c5["tsamp"], f["period_min"], f["period_max"],
+                                            f["bins_min"], f["bins_max"], w], {}))
+    for m, p in [(1, 1), (2, 1), (7, 3), (33, 64), (150, 260), (1023, 34), (1025, 34), (5000, 260), (21474, 240),
+                 (134217, 16), (3000, 17), (777, 4000), (40, 12000), (9, 70000)]:
+        cases.append((f"ffa-{m}x{p}", ["ffa", m, p], {}))
+    for m, p, _ in inputs.FFA_CASES:
+        cases.append((f"ffa-{m}x{p}", ["ffa", m, p], {}))
+    return cases
+
+
+def test_asan_schedule_check():
+    """The host planner and the C ABI's host-only entry points under
+    AddressSanitizer + UBSan (`make -C riptide_amd/csrc asan`): the period
+    grid, the pass schedule with every unit blob / DMA segment table /
+    row-slot table (validate_exec_plan), and the ladder choice, for the five
+    BASELINE configurations (cfg2 also at bench.py's one-group budget), and
+    the single-transform schedules of every ffa2 shape the GPU parity tests
+    run.  Any sanitizer report aborts the checker (exit status != 0)."""
+    import subprocess
+    from concurrent.futures import ThreadPoolExecutor
+    exe = os.path.join(REPO, "build", "asan", "sched_check")
+    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "riptide_amd", "csrc"), "asan"])
+    env0 = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:exitcode=99",
+                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    # ffa shapes whose rows are too wide for the LDS engine (p > 45 x 64
+    # bins) take the global-memory path: rt_ffa_schedule_check rejects them
+
+    def run(case):
+        name, argv, extra = case
+        env = dict(env0, **extra)
+        env.pop("RIPTIDE_AMD_SCRATCH_MFLOATS", None) if not extra else None
+        r = subprocess.run([exe] + [str(a) for a in argv], env=env, capture_output=True, text=True, timeout=600)
+        return name, argv, r
+
+    cases = _asan_cases()
+    with ThreadPoolExecutor(max_workers=min(6, os.cpu_count() or 2)) as ex:
+        results = list(ex.map(run, cases))
+    for name, argv, r in results:
+        assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, (name, r.stderr[-3000:])
+        if argv[0] == "ffa" and argv[2] > 45 * 64:
+            assert r.returncode == 1 and "bad shape" in r.stdout, (name, r.stdout, r.stderr[-2000:])
+            continue
+        assert r.returncode == 0, (name, r.returncode, r.stdout, r.stderr[-3000:])
+        if name == "cfg2-bench-1536M":
+            assert "launches=14 " in r.stdout, r.stdout

@@ -1,0 +1,132 @@
+#!/bin/bash
+# One parameterised GPU-box runner (repo root, via gpurun) for every
+# measurement this repo makes.  Each step runs under its own time limit and
+# the first failure ends the script (no retries).  Output: gpurun_out/TAG/.
+#
+#   bash tools/gpu_run.sh TAG tests                 GPU parity tests + smoke
+#   bash tools/gpu_run.sh TAG bench [ARGS...]        bench.py (cfg2 headline unless --workload)
+#   bash tools/gpu_run.sh TAG prof                   rocprofv3 kernel-trace summary of the cfg2 bench
+#   bash tools/gpu_run.sh TAG pmc [CFG]              PMC passes (4 counter groups) -> profiles/TAG_pmc_cone[_CFG].json
+#   bash tools/gpu_run.sh TAG configs [LIB...]       per-config table (tools/bench_configs.py) per library
+#   bash tools/gpu_run.sh TAG ab CFG LIB...          same-box A/B of builds: cone ms per trial, alternated twice
+#   bash tools/gpu_run.sh TAG flags CFG FLAGS...     same-box A/B of RIPTIDE_AMD_CONE_FLAGS values
+#   bash tools/gpu_run.sh TAG stamps CFG             per-phase stamps (libriptide_amd_stamps.so)
+#   bash tools/gpu_run.sh TAG round                  round-end pass: pmc (cfg2, cfg3), tests, smoke,
+#                                                    bench cfg2 / cfg3 / cfg5, configs, prof
+set -o pipefail
+TAG=$1; CMD=$2; shift 2
+R=$(pwd)
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+LIB=riptide_amd/libriptide_amd.so
+PMC_GROUPS=(
+  "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"
+  "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU"
+  "FETCH_SIZE"
+  "WRITE_SIZE")
+
+fail() { echo "$1 failed"; tail -25 "$2"; exit 1; }
+
+do_tests() {
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread > "$O/gpu_tests.log" 2>&1 \
+    || { grep -E "FAIL|Error|assert" "$O/gpu_tests.log" | head -30; exit 1; }
+  tail -1 "$O/gpu_tests.log"
+  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || fail smoke "$O/smoke.log"
+  tail -1 "$O/smoke.log"
+}
+
+do_bench() {   # $1: log name, rest: bench.py arguments
+  local name=$1; shift
+  timeout -k 10 900 python -u bench.py "$@" > "$O/$name.log" 2>&1 || fail "bench $*" "$O/$name.log"
+  tail -1 "$O/$name.log" | cut -c1-700
+}
+
+do_prof() {
+  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -f csv \
+     -- python3 "$R/bench.py" --no-cpu-baseline > "$O/bench_prof.log" 2>&1) || fail rocprof "$O/bench_prof.log"
+  tail -1 "$O/bench_prof.log" | cut -c1-300
+  find "$O/prof" -name '*stats*'
+}
+
+do_pmc() {     # $1: cfg2 (bench.py, 2 trials) or a config name (tools/ab_flags.py, 64 trials)
+  local cfg=${1:-cfg2} d="$O/pmc_$1" i=0
+  mkdir -p "$d"
+  for grp in "${PMC_GROUPS[@]}"; do
+    i=$((i+1))
+    if [ "$cfg" = cfg2 ]; then
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace -f csv -d "$d/p$i" -o run \
+         -- python3 "$R/bench.py" --steps 1 --warmup 1 --batch 2 --no-cpu-baseline > "$d/p$i.log" 2>&1) \
+        || fail "pmc pass $i" "$d/p$i.log"
+    else
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace -f csv -d "$d/p$i" -o run \
+         -- python3 "$R/tools/ab_flags.py" 7 "$cfg" > "$d/p$i.log" 2>&1) || fail "pmc pass $i" "$d/p$i.log"
+    fi
+  done
+  local out=profiles/${TAG}_pmc_cone.json
+  [ "$cfg" = cfg2 ] || out=profiles/${TAG}_pmc_cone_$cfg.json
+  local per=4; [ "$cfg" = cfg2 ] || per=64
+  python3 tools/pmc_to_json.py "$d" "$out" $per --config "$cfg" > "$d/json.log" 2>&1 || fail pmc_to_json "$d/json.log"
+  cp "$out" "$O/"
+  echo "pmc $cfg ok: $(head -c 300 "$d/json.log")"
+}
+
+do_configs() {
+  local libs=("$@"); [ ${#libs[@]} -gt 0 ] || libs=($LIB)
+  for lib in "${libs[@]}"; do
+    local n=$(basename "$lib" .so)
+    RIPTIDE_AMD_LIB=$lib timeout -k 10 500 python -u tools/bench_configs.py > "$O/configs_$n.jsonl" 2> "$O/configs_$n.err" \
+      || fail "configs $n" "$O/configs_$n.err"
+    echo "== $n"; cut -c1-220 "$O/configs_$n.jsonl"
+  done
+}
+
+do_ab() {      # CFG LIB...
+  local cfg=$1; shift
+  for rep in 1 2; do
+    for lib in "$@"; do
+      local r
+      r=$(RIPTIDE_AMD_LIB=$lib timeout -k 10 200 python -u tools/ab_env.py RIPTIDE_AMD_CONE_FLAGS 7 "$cfg" 2>&1 | grep '"round": 1') \
+        || { echo "$lib failed"; exit 1; }
+      echo "$(basename "$lib") $r" | tee -a "$O/ab_$cfg.log"
+    done
+  done
+}
+
+do_flags() {   # CFG FLAGS...
+  local cfg=$1; shift
+  for rep in 1 2; do
+    for f in "$@"; do
+      local r
+      r=$(timeout -k 10 200 python -u tools/ab_flags.py "$f" "$cfg" 2>&1 | tail -1) || { echo "flags $f failed"; exit 1; }
+      echo "flags=$f $r" | tee -a "$O/flags_$cfg.log"
+    done
+  done
+}
+
+do_stamps() {
+  local cfg=${1:-cfg2}
+  RIPTIDE_AMD_LIB=riptide_amd/libriptide_amd_stamps.so timeout -k 10 300 python -u tools/diag_stamps.py 4 "$cfg" \
+    > "$O/stamps_$cfg.json" 2> "$O/stamps_$cfg.err" || fail "stamps $cfg" "$O/stamps_$cfg.err"
+  cut -c1-1500 "$O/stamps_$cfg.json"
+}
+
+case "$CMD" in
+  tests) do_tests ;;
+  bench) do_bench bench "$@" ;;
+  prof) do_prof ;;
+  pmc) do_pmc "${1:-cfg2}" ;;
+  configs) do_configs "$@" ;;
+  ab) do_ab "$@" ;;
+  flags) do_flags "$@" ;;
+  stamps) do_stamps "$@" ;;
+  round)
+    do_pmc cfg2
+    do_pmc cfg3
+    do_tests
+    do_bench bench
+    do_bench bench_cfg3 --workload cfg3
+    do_bench bench_cfg5 --workload cfg5
+    do_configs
+    do_prof ;;
+  *) echo "unknown command $CMD"; exit 2 ;;
+esac

@@ -4,9 +4,10 @@ the cone kernel from FETCH_SIZE / WRITE_SIZE (rocprofv3, KB units), with the
 gfx950 correction of MI355X_MICROARCH.md (FETCH_SIZE reports half the bytes of
 wide streaming reads: x2), plus the SQ counters as ratios.
 
-usage: tools/pmc_to_json.py gpurun_out/<pmc tag> profiles/<name>.json TRIALS
-(TRIALS = trials the profiled bench processed: gpu_pmc.sh runs warmup 1 +
-steps 1 at batch 2 -> 4)
+usage: tools/pmc_to_json.py gpurun_out/<pmc dir> profiles/<name>.json TRIALS [--config CFG]
+(TRIALS = trials the profiled run processed: tools/gpu_run.sh pmc cfg2 runs
+bench.py warmup 1 + steps 1 at batch 2 -> 4; pmc CFG runs tools/ab_flags.py,
+2 rounds x 4 runs x 8 trials -> 64)
 """
 import csv
 import glob
@@ -19,6 +20,7 @@ from collections import defaultdict
 
 def main():
     root, out, trials = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    config = sys.argv[sys.argv.index("--config") + 1] if "--config" in sys.argv else "cfg2"
     sums = defaultdict(float)
     disp = defaultdict(set)
     for f in sorted(glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True)):
@@ -36,6 +38,7 @@ def main():
     from bench import source_digest
     res = {
         "kernel": "cone_kernel",
+        "config": config,
         "source": root,
         "commit": commit,
         "csrc_sha": source_digest(),      # bench.py uses the summary only for these exact kernel sources
