@@ -269,7 +269,7 @@ void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStrea
             r.moved = L.moved_bytes * batch;
             ck(hipEventRecord(r.a, s), "hipEventRecord");
         }
-        ck(launch_cone(a, L.smax, L.rw, L.wide_snr != 0, s), "cone_kernel");
+        ck(launch_cone(a, L.smax, L.rw, L.wide_snr != 0, L.snr != 0, s), "cone_kernel");
         if (prof) {
             ck(hipEventRecord(r.b, s), "hipEventRecord");
             std::lock_guard<std::mutex> lk(g_prof.mu);

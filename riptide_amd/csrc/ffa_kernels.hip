@@ -2122,10 +2122,13 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
 // two workgroups per CU: a unit's DMA is waited for at its start, the CU's
 // other workgroup filling the wait.
 //   begin(u) [DMA] | wait | merge(u) | store or S/N(u)
+// SNR: the launch's units all end in the fused S/N (final passes) -- or none
+// does (the merge-only passes store their output level): separate instances,
+// so a merge-only launch carries no S/N code and no S/N register floor.
 // WIDE: final units whose S/N takes the widths past its register window as
 // plain LDS windows (snr_wide_ok; a separate instantiation, so the plans
 // without such widths run code without it)
-template <int SMAX, int RWT = 0, bool WIDE = false>
+template <int SMAX, int RWT, bool WIDE, bool SNR>
 __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(ConeArgs a)
 {
     constexpr int RW = RWT ? RWT : merge_rows_per_wave(SMAX);   // register rows per wave
@@ -2164,9 +2167,12 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
     const int p = U.p;
     const int L = U.levels;
     float* const buf = data;
+    // the launch kind is the unit's (the planner splits final and merge-only
+    // launches; validate_exec_plan)
+    ok = ok && ((U.dst == kSelSnr) == SNR);
     // a final pass's per-width S/N constants, published by the barrier below
     // (the S/N row passes have no barrier of their own)
-    if (U.dst == kSelSnr && tid < (int)a.num_widths) snr_width_consts(wl[tid], p, whb + 2 * tid);
+    if (SNR && tid < (int)a.num_widths) snr_width_consts(wl[tid], p, whb + 2 * tid);
     // the roll table of a 4-slot unit (past its blob's LDS part, which the
     // DMA may still be writing), published by the barrier below
     if constexpr (SMAX == 4)
@@ -2185,7 +2191,7 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
         // merge levels, deepest first; a non-final pass stores its output
         // level straight from registers (st), a final pass keeps it in LDS
         // for the S/N epilogue
-        const bool st = U.dst != kSelSnr;
+        constexpr bool st = !SNR;
         const bool st_regs = st && (a.flags & kConeStoreFromRegs);
         const float* dst = (U.dst == kSelPing ? a.ping : a.pong) + (uint64_t)U.trial * a.buf_stride + U.buf_off;
         const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(dst, (((uint32_t)U.m * (uint32_t)p + 3u) & ~3u) * 4u);
@@ -2235,7 +2241,7 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
                         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(obase[r * qst + j]), rs,
                                                               (int)(o0 + (uint32_t)(r * p + j) * 4u), 0, kStoreCpol);
             }
-        } else {
+        } else if constexpr (SNR) {
 #ifdef RT_STAMPS
             if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(a, U, obase, qout, wl, n0, tid, whb, tl);
 #else
@@ -2272,56 +2278,64 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
 // One workgroup per unit: the hardware dispatcher keeps both of a CU's
 // workgroup slots busy to the end of the launch (measured: 10.37 vs 11.55 ms
 // per cfg2 trial against a persistent grid, round 1).
-hipError_t launch_cone(const ConeArgs& args, uint32_t smax, uint32_t rw, bool wide_snr, hipStream_t s)
+template <int SMAX, int RW = 0>
+static hipError_t launch_kind(const ConeArgs& args, dim3 g, dim3 b, bool wide_snr, bool snr, hipStream_t s)
+{
+    if (!snr) {
+        if (wide_snr) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((cone_kernel<SMAX, RW, false, false>), g, b, 0, s, args);
+    } else if (wide_snr) {
+        if constexpr (SMAX >= 3 && SMAX <= 5 && RW == 0) hipLaunchKernelGGL((cone_kernel<SMAX, 0, true, true>), g, b, 0, s, args);
+        else return hipErrorInvalidValue;
+    } else {
+        hipLaunchKernelGGL((cone_kernel<SMAX, RW, false, true>), g, b, 0, s, args);
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_cone(const ConeArgs& args, uint32_t smax, uint32_t rw, bool wide_snr, bool snr, hipStream_t s)
 {
     if (!args.num_items || !args.batch) return hipSuccess;
     const uint64_t total = (uint64_t)args.num_items * args.batch;
     if (total > 0xFFFFFFFFull) return hipErrorInvalidValue;
     const dim3 g((uint32_t)total), b(kConeBlock);
+    hipError_t e = hipErrorInvalidValue;
     switch (smax) {
     case 1:
         switch (rw) {
-        case 12: hipLaunchKernelGGL((cone_kernel<1, 12>), g, b, 0, s, args); break;
-        case 16: hipLaunchKernelGGL((cone_kernel<1, 16>), g, b, 0, s, args); break;
-        case 20: hipLaunchKernelGGL((cone_kernel<1, 20>), g, b, 0, s, args); break;
-        default: hipLaunchKernelGGL(cone_kernel<1>, g, b, 0, s, args); break;
+        case 12: e = launch_kind<1, 12>(args, g, b, wide_snr, snr, s); break;
+        case 16: e = launch_kind<1, 16>(args, g, b, wide_snr, snr, s); break;
+        case 20: e = launch_kind<1, 20>(args, g, b, wide_snr, snr, s); break;
+        default: e = launch_kind<1>(args, g, b, wide_snr, snr, s); break;
         }
         break;
-    case 2: hipLaunchKernelGGL(cone_kernel<2>, g, b, 0, s, args); break;
-    case 3:
-        if (wide_snr) hipLaunchKernelGGL((cone_kernel<3, 0, true>), g, b, 0, s, args);
-        else hipLaunchKernelGGL(cone_kernel<3>, g, b, 0, s, args);
-        break;
+    case 2: e = launch_kind<2>(args, g, b, wide_snr, snr, s); break;
+    case 3: e = launch_kind<3>(args, g, b, wide_snr, snr, s); break;
     case 4:
         switch (rw) {
-        case 5: hipLaunchKernelGGL((cone_kernel<4, 5>), g, b, 0, s, args); break;
-        case 6: hipLaunchKernelGGL((cone_kernel<4, 6>), g, b, 0, s, args); break;
-        case 7: hipLaunchKernelGGL((cone_kernel<4, 7>), g, b, 0, s, args); break;
-        case 8: hipLaunchKernelGGL((cone_kernel<4, 8>), g, b, 0, s, args); break;
-        default:
-            if (wide_snr) hipLaunchKernelGGL((cone_kernel<4, 0, true>), g, b, 0, s, args);
-            else hipLaunchKernelGGL(cone_kernel<4>, g, b, 0, s, args);
-            break;
+        case 5: e = launch_kind<4, 5>(args, g, b, wide_snr, snr, s); break;
+        case 6: e = launch_kind<4, 6>(args, g, b, wide_snr, snr, s); break;
+        case 7: e = launch_kind<4, 7>(args, g, b, wide_snr, snr, s); break;
+        case 8: e = launch_kind<4, 8>(args, g, b, wide_snr, snr, s); break;
+        default: e = launch_kind<4>(args, g, b, wide_snr, snr, s); break;
         }
         break;
     case 5:
         switch (rw) {
-        case 5: hipLaunchKernelGGL((cone_kernel<5, 5>), g, b, 0, s, args); break;
-        case 6: hipLaunchKernelGGL((cone_kernel<5, 6>), g, b, 0, s, args); break;
-        case 7: hipLaunchKernelGGL((cone_kernel<5, 7>), g, b, 0, s, args); break;
-        case 8: hipLaunchKernelGGL((cone_kernel<5, 8>), g, b, 0, s, args); break;
-        default:
-            if (wide_snr) hipLaunchKernelGGL((cone_kernel<5, 0, true>), g, b, 0, s, args);
-            else hipLaunchKernelGGL(cone_kernel<5>, g, b, 0, s, args);
-            break;
+        case 5: e = launch_kind<5, 5>(args, g, b, wide_snr, snr, s); break;
+        case 6: e = launch_kind<5, 6>(args, g, b, wide_snr, snr, s); break;
+        case 7: e = launch_kind<5, 7>(args, g, b, wide_snr, snr, s); break;
+        case 8: e = launch_kind<5, 8>(args, g, b, wide_snr, snr, s); break;
+        default: e = launch_kind<5>(args, g, b, wide_snr, snr, s); break;
         }
         break;
-    case 8: hipLaunchKernelGGL(cone_kernel<8>, g, b, 0, s, args); break;
-    case 16: hipLaunchKernelGGL(cone_kernel<16>, g, b, 0, s, args); break;
-    case kMaxSlots: hipLaunchKernelGGL(cone_kernel<kMaxSlots>, g, b, 0, s, args); break;
-    case kPack2: hipLaunchKernelGGL(cone_kernel<kPack2>, g, b, 0, s, args); break;
+    case 8: e = launch_kind<8>(args, g, b, wide_snr, snr, s); break;
+    case 16: e = launch_kind<16>(args, g, b, wide_snr, snr, s); break;
+    case kMaxSlots: e = launch_kind<kMaxSlots>(args, g, b, wide_snr, snr, s); break;
+    case kPack2: e = launch_kind<kPack2>(args, g, b, wide_snr, snr, s); break;
     default: return hipErrorInvalidValue;
     }
+    if (e != hipSuccess) return e;
     return hipGetLastError();
 }
 

@@ -45,7 +45,8 @@ hipError_t launch_downsample_ladder(const float* x, uint64_t n_in, uint64_t x_st
 hipError_t launch_downsample_fused(const float* x, uint64_t n_in, uint64_t x_stride, const DsRung* d_rungs,
                                    uint32_t num_rungs, float* out, uint64_t out_stride, uint32_t batch, hipStream_t s);
 // smax: merge_slots() bucket covering every transform of the launch
-hipError_t launch_cone(const ConeArgs& args, uint32_t smax, uint32_t rw, bool wide_snr, hipStream_t s);   // grid (num_items, batch); rw: Launch::rw
+hipError_t launch_cone(const ConeArgs& args, uint32_t smax, uint32_t rw, bool wide_snr, bool snr,
+                       hipStream_t s);   // grid (num_items, batch); rw, wide_snr, snr: the Launch's
 hipError_t launch_ffa_level(const float* in, float* out, const uint2* d_nodes, uint32_t num_nodes,
                             uint32_t rows, uint32_t p, hipStream_t s);
 

@@ -348,8 +348,11 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
         std::sort(buckets.begin(), buckets.end());
         buckets.erase(std::unique(buckets.begin(), buckets.end()), buckets.end());
         for (uint32_t k = 0; k < gpasses; ++k) {
-            for (const int bucket : buckets) {
+            // merge-only and final (fused S/N) units in separate launches, so
+            // each runs a kernel instance without the other's code
+            for (const int bucket : buckets) for (int fin = 0; fin < 2; ++fin) {
                 Launch L;
+                L.snr = (uint32_t)fin;
                 L.smax = (uint32_t)bucket;
                 L.first = (uint32_t)out.items.size();
                 L.group = group;
@@ -361,6 +364,7 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
                     const FfaXform& X = out.xf[i];
                     const uint8_t src = k == 0 ? kSelLeaves : (((P - k) % 2 == 0) ? kSelPing : kSelPong);
                     const bool last = (k == P - 1);
+                    if ((last && snr_epilogue) != (fin == 1)) continue;
                     const uint8_t dst = last ? (snr_epilogue ? kSelSnr : kSelPing)
                                              : (((P - 1 - k) % 2 == 0) ? kSelPing : kSelPong);
                     for (ConeItem it : sp[k].items) {
@@ -971,6 +975,9 @@ void validate_exec_plan(const ExecPlan& ex, bool snr_epilogue)
             } else if (it.mode == kModeTile && (need.entries > kDescEntries || it.pad == kNoBlob)) {
                 throw std::runtime_error("schedule: tile descriptor table exceeds its LDS area");
             }
+            // the launch's kernel instance is the unit's kind (final: fused S/N)
+            if ((it.dst == kSelSnr) != (L.snr != 0)) throw std::runtime_error("schedule: unit in a launch of the other kind");
+            if (L.wide_snr && !L.snr) throw std::runtime_error("schedule: wide S/N on a merge-only launch");
             // the launch's kernel instance stages enough register rows for every level
             const int rw = L.rw ? (int)L.rw : merge_rows_per_wave((int)L.smax);
             if (it.pad != kNoBlob) {

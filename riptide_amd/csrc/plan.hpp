@@ -54,6 +54,7 @@ struct Launch {
     uint32_t smax = 0;               // cone kernel variant: merge_slots() of every transform in the launch
     uint32_t rw = 0;                 // register rows per wave of the variant (0: merge_rows_per_wave(smax))
     uint32_t wide_snr = 0;           // final units whose S/N reads wide widths as plain LDS windows (WIDE variant)
+    uint32_t snr = 0;                // 1: every unit ends in the fused S/N (a final pass); 0: none does
     double alg_bytes = 0;            // 4mp read + (4mp | 4*rows_eval*W) write
     double moved_bytes = 0;          // bytes the items actually read + write (cone overlap incl.)
     uint64_t cells = 0;              // sum m*p of the transforms in this launch

@@ -11,6 +11,8 @@
 #   bash tools/gpu_run.sh TAG ab CFG LIB...          same-box A/B of builds: cone ms per trial, alternated twice
 #   bash tools/gpu_run.sh TAG flags CFG FLAGS...     same-box A/B of RIPTIDE_AMD_CONE_FLAGS values
 #   bash tools/gpu_run.sh TAG stamps CFG             per-phase stamps (libriptide_amd_stamps.so)
+#   bash tools/gpu_run.sh TAG trace LIB...           per-launch cone durations of the cfg2 bench per library
+#   bash tools/gpu_run.sh TAG parity LIB...          GPU parity tests (test_gpu_parity.py) per library
 #   bash tools/gpu_run.sh TAG round                  round-end pass: pmc (cfg2, cfg3), tests, smoke,
 #                                                    bench cfg2 / cfg3 / cfg5, configs, prof
 set -o pipefail
@@ -110,6 +112,28 @@ do_stamps() {
   cut -c1-1500 "$O/stamps_$cfg.json"
 }
 
+do_trace() {
+  for lib in "$@"; do
+    local n=$(basename "$lib" .so)
+    (cd /tmp && export TMPDIR=/tmp && RIPTIDE_AMD_LIB=$R/$lib timeout -k 10 400 rocprofv3 --kernel-trace -d "$O/trace_$n" \
+       -o run -f csv -- python3 "$R/bench.py" --no-cpu-baseline --steps 4 > "$O/trace_$n.log" 2>&1) \
+      || fail "trace $n" "$O/trace_$n.log"
+    echo "== $n: $(tail -1 "$O/trace_$n.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["value"],2), "trials/s", d["config"]["cone_launches_per_step"], "launches", "checked", d.get("checked"))')"
+    python3 tools/prof_dispatch.py "$O/trace_$n" \
+      "$(tail -1 "$O/trace_$n.log" | python3 -c 'import json,sys; print(json.loads(sys.stdin.read())["config"]["cone_launches_per_step"])')" \
+      | tee "$O/trace_$n.txt"
+  done
+}
+
+do_parity() {
+  for lib in "$@"; do
+    local n=$(basename "$lib" .so)
+    RIPTIDE_AMD_LIB=$R/$lib timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 240 \
+      --timeout-method thread > "$O/parity_$n.log" 2>&1 || { echo "$n parity FAILED"; grep -E "FAIL|Error|assert" "$O/parity_$n.log" | head -20; exit 1; }
+    echo "$n parity: $(tail -1 "$O/parity_$n.log")"
+  done
+}
+
 case "$CMD" in
   tests) do_tests ;;
   bench) do_bench bench "$@" ;;
@@ -119,6 +143,8 @@ case "$CMD" in
   ab) do_ab "$@" ;;
   flags) do_flags "$@" ;;
   stamps) do_stamps "$@" ;;
+  trace) do_trace "$@" ;;
+  parity) do_parity "$@" ;;
   round)
     do_pmc cfg2
     do_pmc cfg3
