@@ -8,6 +8,7 @@
 // bit-identical to the strict restatement of downsample.hpp:44-82.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.hpp"
@@ -1388,10 +1389,10 @@ __device__ __forceinline__ void put_tasks(float* base, int q, const float (&v)[k
 // Each level's outputs are staged in registers between two barriers, then
 // written back.  With `st` set (a non-final pass), the output level goes from
 // the staging registers straight to global memory instead of back into LDS.
-template <int SMAX, int RW>
+template <int SMAX, int RW, class PreStore>
 __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int p, int L, int tid, bool st,
                                              __amdgpu_buffer_rsrc_t rs, uint32_t st_o0, uint32_t flags, float* dummy,
-                                             int qout)
+                                             int qout, PreStore&& pre_store)
 {
     const int lane = tid & 63, wave = tid >> 6;
     const bool tile = C.tile;
@@ -1425,6 +1426,7 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
                 }
                 l = lo - 1;
                 if (lo == 0 && st) {
+                    pre_store();
                     put_tasks<true>(base, qs, v, p, tid, nrows, rs, st_o0);
                     return;
                 }
@@ -1451,6 +1453,7 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
             }
             l = lo - 1;
             if (lo == 0 && st) {
+                pre_store();
                 store_rows_lanes<RW>(v, p, lane, wave, nrows, rs, st_o0);
                 return;
             }
@@ -1476,6 +1479,7 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
                 else merge_step_slots<SMAX, RW, false>(C, src, p, lo, lane, wave, v, lo_src, sw, nq);
                 l = lo - 1;
                 if (lo == 0 && st) {
+                    pre_store();
                     store_rows_slots<SMAX, RW>(v, p, lane, sw, nq, rs, st_o0);
                     return;
                 }
@@ -1508,6 +1512,7 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
             merge_level_dense<S, RW, false>(C, src, p, l, lane, wave, nr, v, lo_src);
         l = lo - 1;
         if (lo == 0 && st) {
+            pre_store();
             store_rows<S, RW>(v, p, lane, wave, nr, rs, st_o0);
             return;
         }
@@ -2117,11 +2122,17 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
 #endif
 
 // One kernel per merge slot width SMAX (units with ceil(p/64) <= SMAX), so each
-// gets its own register allocation; one workgroup per unit u = blockIdx.x
-// (unit u = item u / batch, trial u % batch; items are sorted longest first),
-// two workgroups per CU: a unit's DMA is waited for at its start, the CU's
-// other workgroup filling the wait.
-//   begin(u) [DMA] | wait | merge(u) | store or S/N(u)
+// gets its own register allocation.  Two workgroups per CU; workgroup b runs
+// units u = b, b + G, b + 2G, ... (G = gridDim.x; unit u = item u / batch,
+// trial u % batch; items are sorted longest first, so every workgroup's
+// share is alike).  With G = the number of units (one unit per workgroup) the
+// hardware dispatcher starts each unit; with a persistent grid (2 per CU,
+// kConePersist) a workgroup starts its next unit itself, as soon as the
+// current one no longer reads its LDS level buffer: a merge-only unit
+// stores its output level straight from registers, so the next unit's
+// record, DMA segments and bottom-level fill are issued just before that
+// store and land while it drains.
+//   begin(u) | wait | merge(u) .. last step | begin(u + G) | store(u) | wait | merge(u + G) ..
 // SNR: the launch's units all end in the fused S/N (final passes) -- or none
 // does (the merge-only passes store their output level): separate instances,
 // so a merge-only launch carries no S/N code and no S/N register floor.
@@ -2141,143 +2152,184 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
 
     const int tid = threadIdx.x;
 #ifdef RT_STAMPS
-    const unsigned long long t_entry = __builtin_amdgcn_s_memtime();
-    const unsigned long long r_entry = __builtin_amdgcn_s_memrealtime();
+    unsigned long long t_entry = __builtin_amdgcn_s_memtime();
+    unsigned long long r_entry = __builtin_amdgcn_s_memrealtime();
     unsigned long long t_begin[3] = {};
 #endif
     const uint32_t total = a.num_items * a.batch;
-    if (blockIdx.x >= total) return;
-    const uint32_t u = blockIdx.x;
+    uint32_t u = blockIdx.x;
+    if (u >= total) return;
     if (tid < (int)a.num_widths) wl[tid] = (int)a.widths[tid];   // visible after the first barrier
     if (tid == 0) {
         uint32_t wm = 0;
         for (uint32_t i = 0; i < a.num_widths; ++i) wm = max(wm, a.widths[i]);
         wl[kMaxWidths] = (int)wm;
     }
-    const bool dma = !(a.flags & kConeDiagNoLand);
-    bool ok;
-#ifdef RT_STAMPS
-    const UnitCtx C = unit_begin<SMAX, RW>(a, u, aux, data, tid, dma, ok, t_begin);
-    unsigned long long tl[kStampMarks] = {};
-    tl[0] = __builtin_amdgcn_s_memtime();
-#else
-    const UnitCtx C = unit_begin<SMAX, RW>(a, u, aux, data, tid, dma, ok);
-#endif
-    const UnitView& U = C.U;
-    const int p = U.p;
-    const int L = U.levels;
     float* const buf = data;
-    // the launch kind is the unit's (the planner splits final and merge-only
-    // launches; validate_exec_plan)
-    ok = ok && ((U.dst == kSelSnr) == SNR);
-    // a final pass's per-width S/N constants, published by the barrier below
-    // (the S/N row passes have no barrier of their own)
-    if (SNR && tid < (int)a.num_widths) snr_width_consts(wl[tid], p, whb + 2 * tid);
-    // the roll table of a 4-slot unit (past its blob's LDS part, which the
-    // DMA may still be writing), published by the barrier below
-    if constexpr (SMAX == 4)
-        if (C.slots && ok) build_roll_lut4(aux + kLut4Off, p, tid);
-    // the short-row roll table in the unused metadata area
-    if constexpr (SMAX == kPack2)
-        if (ok && p >= kPackSeg) build_pack_lut(aux, p, tid);
-    // every wave waits for its own DMA, the barrier publishes all of them
-    __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)
-    lds_barrier();
-    RT_MARK(1);
-    RT_MARK(2);
-    if (!ok) {
-        if (tid == 0 && a.error_flag) atomicOr(a.error_flag, 1);
-    } else {
-        // merge levels, deepest first; a non-final pass stores its output
-        // level straight from registers (st), a final pass keeps it in LDS
-        // for the S/N epilogue
-        constexpr bool st = !SNR;
-        const bool st_regs = st && (a.flags & kConeStoreFromRegs);
-        const float* dst = (U.dst == kSelPing ? a.ping : a.pong) + (uint64_t)U.trial * a.buf_stride + U.buf_off;
-        const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(dst, (((uint32_t)U.m * (uint32_t)p + 3u) & ~3u) * 4u);
-        const uint32_t o0 = (uint32_t)(U.node_start + U.s0) * (uint32_t)p * 4u;
-        const int n0 = rows_at(C, 0);
-        // a final pass's output level at a row stride = 16 (mod 32): the
-        // S/N epilogue's lane groups (two rows of 16 lanes per 32-lane LDS
-        // group, odd chunk strides) then read and write on distinct banks
-        // (at stride p they collided on up to 10 of 32 banks)
-        int qout = p;
-        // short rows in (row, segment) tasks: every level above the fill at
-        // the odd stride pack_stride(p)
+    // the launch's arguments re-read (scalar loads from the kernarg segment)
+    // in every unit, through a pointer the compiler cannot see is invariant:
+    // nothing per launch or per unit is hoisted out of the unit loop into
+    // long-lived (spilled) SGPRs.  Only u is carried from one unit to the next.
+    typedef const __attribute__((address_space(4))) ConeArgs* kargs_ptr;
+    const kargs_ptr kp = (kargs_ptr)__builtin_amdgcn_kernarg_segment_ptr();
+    bool first = true;
+    for (;;) {
+        kargs_ptr kpl = kp;
+        asm volatile("" : "+s"(kpl));
+        const ConeArgs& A = *(const ConeArgs*)kpl;
+        const bool dma = !(A.flags & kConeDiagNoLand);
+        bool ok;
+        // the first unit's DMA is issued here; every later unit's was issued
+        // by begin_next of the unit before (this call re-reads its record)
+#ifdef RT_STAMPS
+        UnitCtx C = unit_begin<SMAX, RW>(A, u, aux, data, tid, dma && first, ok, first ? t_begin : nullptr);
+        unsigned long long tl[kStampMarks] = {};
+        tl[0] = __builtin_amdgcn_s_memtime();
+#else
+        UnitCtx C = unit_begin<SMAX, RW>(A, u, aux, data, tid, dma && first, ok);
+#endif
+        first = false;
+        const UnitView& U = C.U;
+        const int p = U.p;
+        const int L = U.levels;
+        // the launch kind is the unit's (the planner splits final and merge-
+        // only launches; validate_exec_plan)
+        ok = ok && ((U.dst == kSelSnr) == SNR);
+        // a final pass's per-width S/N constants, published by the barrier
+        // below (the S/N row passes have no barrier of their own)
+        if (SNR && tid < (int)A.num_widths) snr_width_consts(wl[tid], p, whb + 2 * tid);
+        // the roll table of a 4-slot unit (past its blob's LDS part, which
+        // the DMA may still be writing), published by the barrier below
+        if constexpr (SMAX == 4)
+            if (C.slots && ok) build_roll_lut4(aux + kLut4Off, p, tid);
+        // the short-row roll table in the unused metadata area
         if constexpr (SMAX == kPack2)
-            if (L > 0) qout = pack_stride(p);
-        if constexpr (SMAX <= 5 && SMAX != kPack2) {
-            // = 16 (mod 32) and >= p + kSnrMaxChunk (room for the S/N's whole-
-            // chunk prefix writes and its wrapped prefix extension), else >=
-            // p + kSnrWin (the extension only)
-            const int qa = p + kSnrMaxChunk + ((16 - ((p + kSnrMaxChunk) & 31)) & 31);
-            const int qb = p + kSnrWin + ((16 - ((p + kSnrWin) & 31)) & 31);
-            if (!st && L > 0 && C.slots && (a.flags & kConeFuse2) && (a.flags & kConeSnrStride)) {
-                qout = n0 * qa <= kLdsDataFloats ? qa : (n0 * qb <= kLdsDataFloats ? qb : p);
-                // widths past the register window: a stride with room for
-                // their plain-LDS windows (snr_wide_stride), = 16 (mod 32)
-                // where that fits too
-                const int wmax = wl[kMaxWidths];
-                if (WIDE && snr_group(p) == 16 && wmax > kSnrWin && wmax < p) {
-                    const int qw = snr_wide_stride(p, wmax);
-                    const int qwp = qw + ((16 - (qw & 31)) & 31);
-                    if (n0 * qwp <= kLdsDataFloats) qout = qwp;
-                    else if (n0 * qw <= kLdsDataFloats) qout = qw;
+            if (ok && p >= kPackSeg) build_pack_lut(aux, p, tid);
+        // every wave waits for its own DMA (and the previous unit's stores,
+        // which count in the same in-order counter), the barrier publishes
+        // all of them
+        __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)
+        lds_barrier();
+        RT_MARK(1);
+        RT_MARK(2);
+        // the next unit of this workgroup: begun (record, DMA segments, fill
+        // and blob DMA into the level buffer) once every wave is past its
+        // last LDS read of this unit
+        // (final units run one per workgroup: their S/N reads the level
+        // buffer to the end, so the next unit could start only after it)
+        const uint32_t un = u + gridDim.x;
+        const bool has_next = !SNR && un < total;
+        bool begun = false;
+        auto begin_next = [&]() {
+            lds_barrier();                    // the level buffer and metadata area are free
+            if (has_next) {
+                bool ok_next;
+#ifdef RT_STAMPS
+                t_entry = __builtin_amdgcn_s_memtime();
+                (void)unit_begin<SMAX, RW>(A, un, aux, data, tid, dma, ok_next, t_begin);
+#else
+                (void)unit_begin<SMAX, RW>(A, un, aux, data, tid, dma, ok_next);
+#endif
+            }
+            begun = true;
+        };
+        if (!ok) {
+            if (tid == 0 && A.error_flag) atomicOr(A.error_flag, 1);
+        } else {
+            // merge levels, deepest first; a non-final pass stores its output
+            // level straight from registers (st), a final pass keeps it in LDS
+            // for the S/N epilogue
+            constexpr bool st = !SNR;
+            const bool st_regs = st && (A.flags & kConeStoreFromRegs);
+            const float* dst = (U.dst == kSelPing ? A.ping : A.pong) + (uint64_t)U.trial * A.buf_stride + U.buf_off;
+            const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(dst, (((uint32_t)U.m * (uint32_t)p + 3u) & ~3u) * 4u);
+            const uint32_t o0 = (uint32_t)(U.node_start + U.s0) * (uint32_t)p * 4u;
+            const int n0 = rows_at(C, 0);
+            // a final pass's output level at a row stride = 16 (mod 32): the
+            // S/N epilogue's lane groups (two rows of 16 lanes per 32-lane LDS
+            // group, odd chunk strides) then read and write on distinct banks
+            // (at stride p they collided on up to 10 of 32 banks)
+            int qout = p;
+            // short rows in (row, segment) tasks: every level above the fill
+            // at the odd stride pack_stride(p)
+            if constexpr (SMAX == kPack2)
+                if (L > 0) qout = pack_stride(p);
+            if constexpr (SMAX <= 5 && SMAX != kPack2) {
+                // = 16 (mod 32) and >= p + kSnrMaxChunk (room for the S/N's
+                // whole-chunk prefix writes and its wrapped prefix extension),
+                // else >= p + kSnrWin (the extension only)
+                const int qa = p + kSnrMaxChunk + ((16 - ((p + kSnrMaxChunk) & 31)) & 31);
+                const int qb = p + kSnrWin + ((16 - ((p + kSnrWin) & 31)) & 31);
+                if (!st && L > 0 && C.slots && (A.flags & kConeFuse2) && (A.flags & kConeSnrStride)) {
+                    qout = n0 * qa <= kLdsDataFloats ? qa : (n0 * qb <= kLdsDataFloats ? qb : p);
+                    // widths past the register window: a stride with room for
+                    // their plain-LDS windows (snr_wide_stride), = 16 (mod 32)
+                    // where that fits too
+                    const int wmax = wl[kMaxWidths];
+                    if (WIDE && snr_group(p) == 16 && wmax > kSnrWin && wmax < p) {
+                        const int qw = snr_wide_stride(p, wmax);
+                        const int qwp = qw + ((16 - (qw & 31)) & 31);
+                        if (n0 * qwp <= kLdsDataFloats) qout = qwp;
+                        else if (n0 * qw <= kLdsDataFloats) qout = qw;
+                    }
                 }
             }
-        }
-        if (L > 0 && !(a.flags & kConeDiagNoMerge))
-            merge_levels<SMAX, RW>(C, buf, p, L, tid, st_regs, rs, o0, a.flags, buf + kLdsBufFloats + 4 + (tid & 63),
-                                   qout);
-        RT_MARK(3);
-        // the output level: dense rows from the buffer start, or (no merge
-        // level) the single bottom row where the DMA left it
-        float* const obase = L > 0 ? buf : buf + (C.table ? uni(bottom_offsets(C)[0]) : C.al);
-        if (st) {
-            if (L == 0 || !st_regs) {
-                const int qst = L > 0 ? qout : p;    // the merged level's LDS row stride
-                for (int r = 0; r < n0; ++r)
-                    for (int j = tid; j < p; j += kConeBlock)
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(obase[r * qst + j]), rs,
-                                                              (int)(o0 + (uint32_t)(r * p + j) * 4u), 0, kStoreCpol);
-            }
-        } else if constexpr (SNR) {
+            if (L > 0 && !(A.flags & kConeDiagNoMerge))
+                merge_levels<SMAX, RW>(C, buf, p, L, tid, st_regs, rs, o0, A.flags,
+                                       buf + kLdsBufFloats + 4 + (tid & 63), qout, begin_next);
+            RT_MARK(3);
+            // the output level: dense rows from the buffer start, or (no
+            // merge level) the single bottom row where the DMA left it
+            float* const obase = L > 0 ? buf : buf + (C.table ? uni(bottom_offsets(C)[0]) : C.al);
+            if (st) {
+                if (!begun) {
+                    const int qst = L > 0 ? qout : p;    // the merged level's LDS row stride
+                    for (int r = 0; r < n0; ++r)
+                        for (int j = tid; j < p; j += kConeBlock)
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(obase[r * qst + j]), rs,
+                                                                  (int)(o0 + (uint32_t)(r * p + j) * 4u), 0, kStoreCpol);
+                }
+            } else if constexpr (SNR) {
 #ifdef RT_STAMPS
-            if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(a, U, obase, qout, wl, n0, tid, whb, tl);
+                if (!(A.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(A, U, obase, qout, wl, n0, tid, whb, tl);
 #else
-            if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(a, U, obase, qout, wl, n0, tid, whb, nullptr);
+                if (!(A.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(A, U, obase, qout, wl, n0, tid, whb, nullptr);
 #endif
+            }
         }
-    }
+        if (!begun) begin_next();
 #ifdef RT_STAMPS
-    lds_barrier();
-    RT_MARK(4);
-    tl[5] = t_entry;
-    tl[11] = t_begin[0];
-    tl[12] = t_begin[1];
-    tl[13] = t_begin[2];
-    RT_MARK(6);
-    tl[14] = r_entry;
-    tl[15] = __builtin_amdgcn_s_memrealtime();
-    if (tid == 0 && a.stamps) {
-        unsigned long long* e = a.stamps + (uint64_t)kStampRecWords * (uint64_t)u;
-        const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));     // HW_REG_HW_ID
-        const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11));   // HW_REG_XCC_ID
-        e[0] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+        RT_MARK(4);
+        tl[5] = t_entry;
+        tl[11] = t_begin[0];
+        tl[12] = t_begin[1];
+        tl[13] = t_begin[2];
+        RT_MARK(6);
+        tl[14] = r_entry;
+        tl[15] = __builtin_amdgcn_s_memrealtime();
+        r_entry = tl[15];
+        if (tid == 0 && A.stamps) {
+            unsigned long long* e = A.stamps + (uint64_t)kStampRecWords * (uint64_t)u;
+            const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));     // HW_REG_HW_ID
+            const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11));   // HW_REG_XCC_ID
+            e[0] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
 #pragma unroll
-        for (int i = 0; i < kStampMarks; ++i) e[1 + i] = tl[i];
-        e[1 + kStampMarks] = (unsigned long long)p | ((unsigned long long)L << 16) |
-                             ((unsigned long long)U.mode << 24) | ((unsigned long long)rows_at(C, 0) << 32) |
-                             ((unsigned long long)(U.dst == kSelSnr) << 48);
-    }
+            for (int i = 0; i < kStampMarks; ++i) e[1 + i] = tl[i];
+            e[1 + kStampMarks] = (unsigned long long)p | ((unsigned long long)L << 16) |
+                                 ((unsigned long long)U.mode << 24) | ((unsigned long long)rows_at(C, 0) << 32) |
+                                 ((unsigned long long)(U.dst == kSelSnr) << 48);
+        }
 #endif
-    // every DMA was waited for at the unit start, and the unit's global
-    // stores need no wait before the end of the program
+        if (!has_next) break;
+        u = un;
+    }
+    // the last unit's global stores need no wait before the end of the
+    // program; every DMA was waited for at its unit's start
 }
 
-// One workgroup per unit: the hardware dispatcher keeps both of a CU's
-// workgroup slots busy to the end of the launch (measured: 10.37 vs 11.55 ms
-// per cfg2 trial against a persistent grid, round 1).
+// Grid: one workgroup per unit, or (kConePersist, merge-only launches) a
+// persistent grid of two workgroups per CU that start their next unit
+// themselves (cone_kernel).
 template <int SMAX, int RW = 0>
 static hipError_t launch_kind(const ConeArgs& args, dim3 g, dim3 b, bool wide_snr, bool snr, hipStream_t s)
 {
@@ -2298,7 +2350,13 @@ hipError_t launch_cone(const ConeArgs& args, uint32_t smax, uint32_t rw, bool wi
     if (!args.num_items || !args.batch) return hipSuccess;
     const uint64_t total = (uint64_t)args.num_items * args.batch;
     if (total > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    const dim3 g((uint32_t)total), b(kConeBlock);
+    uint64_t grid = total;
+    if ((args.flags & kConePersist) && !snr) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        grid = std::min<uint64_t>(total, (uint64_t)cus * kConeWgsPerCu);
+    }
+    const dim3 g((uint32_t)grid), b(kConeBlock);
     hipError_t e = hipErrorInvalidValue;
     switch (smax) {
     case 1:
