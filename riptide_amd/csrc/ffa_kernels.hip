@@ -2336,9 +2336,10 @@ static hipError_t launch_kind(const ConeArgs& args, dim3 g, dim3 b, bool wide_sn
     if (!snr) {
         if (wide_snr) return hipErrorInvalidValue;
         hipLaunchKernelGGL((cone_kernel<SMAX, RW, false, false>), g, b, 0, s, args);
-    } else if (wide_snr) {
+    } else if (wide_snr && SMAX >= 3 && SMAX <= 5 && RW == 0) {
+        // (the register-row-class instances have no WIDE form: their S/N
+        // reads the wide widths through the general per-width path)
         if constexpr (SMAX >= 3 && SMAX <= 5 && RW == 0) hipLaunchKernelGGL((cone_kernel<SMAX, 0, true, true>), g, b, 0, s, args);
-        else return hipErrorInvalidValue;
     } else {
         hipLaunchKernelGGL((cone_kernel<SMAX, RW, false, true>), g, b, 0, s, args);
     }
