@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <utility>
 #include <cstdlib>
 
 #include "common.hpp"
@@ -372,6 +373,51 @@ __device__ __forceinline__ void dma_run(__amdgpu_buffer_rsrc_t rs, uint32_t goff
     }
 }
 
+// s_waitcnt vmcnt(n) for a wave-uniform n (the immediate of each case): the
+// wave's vector-memory operations other than its n youngest are done; n < 0
+// or beyond the counter's range waits for all of them.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_imm()
+{
+    __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 15) | ((N >> 4) << 14));
+}
+template <int... Ns>
+__device__ __forceinline__ void wait_vmcnt_sw(int n, std::integer_sequence<int, Ns...>)
+{
+    bool done = false;
+    ((n == Ns ? (wait_vmcnt_imm<Ns>(), done = true) : false), ...);
+    if (!done) wait_vmcnt_imm<0>();
+}
+__device__ __forceinline__ void wait_vmcnt_below(int n)
+{
+    wait_vmcnt_sw(uni(n), std::make_integer_sequence<int, 48>{});
+}
+
+// Exclusive prefix sum of v over the 64 lanes of a wave (DPP row shifts,
+// then the row broadcasts; bound_ctrl writes 0 where the source is outside).
+__device__ __forceinline__ int wave_excl_sum(int v, int lane)
+{
+    int x = v;
+    int y = __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);   // row_shr:1
+    x += (lane & 15) >= 1 ? y : 0;
+    y = __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);       // row_shr:2
+    x += (lane & 15) >= 2 ? y : 0;
+    y = __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);       // row_shr:4
+    x += (lane & 15) >= 4 ? y : 0;
+    y = __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);       // row_shr:8
+    x += (lane & 15) >= 8 ? y : 0;
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);     // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);     // row_bcast:31 -> rows 2, 3
+    return x - v;
+}
+
+// Tile units' bottom-level DMA derived from the unit record (1) or read from
+// the blob's host-built segment table (0: one more dependent memory round
+// trip at the unit's start).  A/B knob.
+#ifndef RT_ANALYTIC_FILL
+#define RT_ANALYTIC_FILL 1
+#endif
+
 // Starts unit (item, trial): its view, and (dma) the LDS DMA of its bottom
 // level into `buf` and, for a tile unit, of its blob into `aux`.  Nothing is
 // waited for: the caller waits (vmcnt) and barriers before reading LDS.
@@ -442,7 +488,43 @@ __device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t u, uin
 #ifdef RT_STAMPS
         if (ts) ts[1] = __builtin_amdgcn_s_memtime() + (ok ? 0 : 0);
 #endif
-        if (ok && dma) {
+        if (ok && dma && RT_ANALYTIC_FILL && C.tile) {
+            // the blob's LDS part: the last wave
+            const __amdgpu_buffer_rsrc_t rb = buffer_rsrc(a.blob + U.blob, (uint32_t)words * 4u);
+            if (wave == kConeWaves - 1) dma_run(rb, 0u, words >> 2, (float*)const_cast<uint32_t*>(C.aux), 0, 1, lane);
+            // the bottom level from the record alone: lane j < 2^L derives
+            // range j of the dependency cone (the split tree walked along the
+            // bits of j, head = 0, the planner's range order: build_tile_blob),
+            // its 16-byte-phase run and, by a wave prefix sum, its first LDS
+            // chunk; wave w then issues runs w, w + 8, ... in pieces of <= 64
+            // chunks -- no segment table and its memory round trip
+            const int L = U.levels;
+            uint32_t size = (uint32_t)U.node_size, lo = (uint32_t)U.s0, hi = (uint32_t)U.s1 - 1u,
+                     start = (uint32_t)U.node_start;
+            for (int l = L - 1; l >= 0; --l) {
+                const uint32_t bit = ((uint32_t)lane >> l) & 1u;
+                const uint32_t hs = size >> 1, cs = bit ? size - hs : hs;
+                const float k = merge_coef(cs, size);
+                lo = merge_index(k, lo);
+                hi = merge_index(k, hi);
+                start += bit ? hs : 0u;
+                size = cs;
+            }
+            const uint32_t first = (start + lo) * (uint32_t)p, al = first & 3u;
+            const int nch = lane < (1 << L) ? (int)(((hi - lo + 1u) * (uint32_t)p + al + 3u) >> 2) : 0;
+            const int g0 = (int)((first - al) >> 2);
+            const int cb = wave_excl_sum(nch, lane);
+            for (int j = wave; j < (1 << L); j += kConeWaves) {
+                const int c0 = __builtin_amdgcn_readlane(cb, j);
+                const int n = __builtin_amdgcn_readlane(nch, j);
+                const uint32_t g = (uint32_t)__builtin_amdgcn_readlane(g0, j);
+                for (int c = 0; c < n; c += 64)
+                    if (lane < n - c && 4 * (c0 + min(n, c + 64)) <= kLdsBufFloats && !(a.flags & kConeDiagNoFill))
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                            rs, (__attribute__((address_space(3))) void*)(buf + 4 * (c0 + c)), 16,
+                            (int)((g + (uint32_t)(c + lane)) * 16u), 0, 0, kFillCpol);
+            }
+        } else if (ok && dma) {
             // DMA segments: wave w issues segments w, w + 8, ...; its lane i
             // holds segment w + 8i (one coalesced vector load)
             const uint4* const segs = reinterpret_cast<const uint4*>(a.blob + U.blob + words);
@@ -1082,11 +1164,13 @@ __device__ __forceinline__ void write_rows_slots(float* base, float* dummy, cons
     }
 }
 
+// Returns the wave's number of store instructions (uniform).
 template <int SMAX, int RW>
-__device__ __forceinline__ void store_rows_slots(const float (&v)[RW][SMAX], int p, int lane, uint32_t sw, int nq,
-                                                 __amdgpu_buffer_rsrc_t rs, uint32_t st_o0)
+__device__ __forceinline__ int store_rows_slots(const float (&v)[RW][SMAX], int p, int lane, uint32_t sw, int nq,
+                                                __amdgpu_buffer_rsrc_t rs, uint32_t st_o0)
 {
     const bool tail_ok = lane + 64 * (SMAX - 1) < p;
+    int n = 0;
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
         if (i / 2 < nq) {
@@ -1100,9 +1184,11 @@ __device__ __forceinline__ void store_rows_slots(const float (&v)[RW][SMAX], int
                                                     : (tail_ok ? ob + 256u * (uint32_t)k : 0x80000000u);
                     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs, (int)o, 0, kStoreCpol);
                 }
+                n += SMAX;
             }
         }
     }
+    return n;
 }
 
 // kPack2 merge step (p <= 32; units always with a blob): register row i of
@@ -1352,16 +1438,19 @@ __device__ __forceinline__ void merge_step_tasks(const UnitCtx& C, const float* 
 // S/N identical.
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
+// Returns the wave's number of global store instructions (uniform).
 template <bool GLOBAL>
-__device__ __forceinline__ void put_tasks(float* base, int q, const float (&v)[kPackTasks][kPackSeg], int p, int tid,
-                                          int nrows, __amdgpu_buffer_rsrc_t rs, uint32_t st_o0)
+__device__ __forceinline__ int put_tasks(float* base, int q, const float (&v)[kPackTasks][kPackSeg], int p, int tid,
+                                         int nrows, __amdgpu_buffer_rsrc_t rs, uint32_t st_o0)
 {
     const int segs = pack_segments(p);
     const int ntask = nrows * segs;
     const int wave0 = tid & ~63;
+    int n = 0;
 #pragma unroll
     for (int i = 0; i < kPackTasks; ++i) {
         if (kConeBlock * i + wave0 < ntask) {
+            n += GLOBAL ? kPackSeg / 4 : 0;
             int r, j0;
             pack_task(min(tid + kConeBlock * i, ntask - 1), segs, p, r, j0);
             if constexpr (GLOBAL) {
@@ -1381,6 +1470,7 @@ __device__ __forceinline__ void put_tasks(float* base, int q, const float (&v)[k
             }
         }
     }
+    return n;
 }
 
 // All merge levels of one unit, deepest first, in place in the dense rows
@@ -1389,8 +1479,10 @@ __device__ __forceinline__ void put_tasks(float* base, int q, const float (&v)[k
 // Each level's outputs are staged in registers between two barriers, then
 // written back.  With `st` set (a non-final pass), the output level goes from
 // the staging registers straight to global memory instead of back into LDS.
+// Returns the wave's store instructions issued after pre_store() (a
+// non-final pass's output level from registers), or -1 if not counted.
 template <int SMAX, int RW, class PreStore>
-__device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int p, int L, int tid, bool st,
+__device__ __forceinline__ int merge_levels(const UnitCtx& C, float* base, int p, int L, int tid, bool st,
                                              __amdgpu_buffer_rsrc_t rs, uint32_t st_o0, uint32_t flags, float* dummy,
                                              int qout, PreStore&& pre_store)
 {
@@ -1427,14 +1519,13 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
                 l = lo - 1;
                 if (lo == 0 && st) {
                     pre_store();
-                    put_tasks<true>(base, qs, v, p, tid, nrows, rs, st_o0);
-                    return;
+                    return put_tasks<true>(base, qs, v, p, tid, nrows, rs, st_o0);
                 }
                 if (!(flags & kConeDiagNoBarrier)) lds_barrier();
                 if (!(flags & kConeDiagNoWrite)) put_tasks<false>(base, qs, v, p, tid, nrows, rs, st_o0);
                 if (!(flags & kConeDiagNoBarrier)) lds_barrier();
             }
-            return;
+            return -1;
         }
         for (int l = L - 1; l >= 0;) {
             const bool two = fuse && l >= 1 && (tile || (node_size >> l) >= 2);
@@ -1455,13 +1546,13 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
             if (lo == 0 && st) {
                 pre_store();
                 store_rows_lanes<RW>(v, p, lane, wave, nrows, rs, st_o0);
-                return;
+                return -1;
             }
             if (!(flags & kConeDiagNoBarrier)) lds_barrier();
             if (!(flags & kConeDiagNoWrite)) write_rows_lanes<RW>(base, dummy, v, p, lane, wave, nrows);
             if (!(flags & kConeDiagNoBarrier)) lds_barrier();
         }
-        return;
+        return -1;
     }
     if constexpr (SMAX <= 5) {
         if (C.slots && fuse) {
@@ -1480,8 +1571,7 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
                 l = lo - 1;
                 if (lo == 0 && st) {
                     pre_store();
-                    store_rows_slots<SMAX, RW>(v, p, lane, sw, nq, rs, st_o0);
-                    return;
+                    return store_rows_slots<SMAX, RW>(v, p, lane, sw, nq, rs, st_o0);
                 }
                 if (!(flags & kConeDiagNoBarrier)) lds_barrier();
                 // the output level of a final pass at row stride qout (the S/N's)
@@ -1489,7 +1579,7 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
                     write_rows_slots<SMAX, RW>(base, dummy, v, p, lane, sw, nq, lo == 0 ? qout : p);
                 if (!(flags & kConeDiagNoBarrier)) lds_barrier();
             }
-            return;
+            return -1;
         }
     }
     for (int l = L - 1; l >= 0;) {
@@ -1514,7 +1604,7 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
         if (lo == 0 && st) {
             pre_store();
             store_rows<S, RW>(v, p, lane, wave, nr, rs, st_o0);
-            return;
+            return -1;
         }
         if (!(flags & kConeDiagNoBarrier)) lds_barrier();
         if (!(flags & kConeDiagNoWrite)) {
@@ -1522,6 +1612,7 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
         }
         if (!(flags & kConeDiagNoBarrier)) lds_barrier();
     }
+    return -1;
 }
 
 template <int CTRL>
@@ -2173,6 +2264,7 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
     typedef const __attribute__((address_space(4))) ConeArgs* kargs_ptr;
     const kargs_ptr kp = (kargs_ptr)__builtin_amdgcn_kernarg_segment_ptr();
     bool first = true;
+    int nst = 0;    // the wave's stores issued after the current unit's DMA (-1: not counted)
     for (;;) {
         kargs_ptr kpl = kp;
         asm volatile("" : "+s"(kpl));
@@ -2205,10 +2297,10 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
         // the short-row roll table in the unused metadata area
         if constexpr (SMAX == kPack2)
             if (ok && p >= kPackSeg) build_pack_lut(aux, p, tid);
-        // every wave waits for its own DMA (and the previous unit's stores,
-        // which count in the same in-order counter), the barrier publishes
-        // all of them
-        __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)
+        // every wave waits for its own DMA, the barrier publishes all of it;
+        // the previous unit's stores, issued after this unit's DMA and counted
+        // in the same in-order counter, may stay in flight (vmcnt(nst))
+        wait_vmcnt_below(nst);
         lds_barrier();
         RT_MARK(1);
         RT_MARK(2);
@@ -2221,8 +2313,8 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
         const bool has_next = !SNR && un < total;
         bool begun = false;
         auto begin_next = [&]() {
-            lds_barrier();                    // the level buffer and metadata area are free
             if (has_next) {
+                lds_barrier();                // the level buffer and metadata area are free
                 bool ok_next;
 #ifdef RT_STAMPS
                 t_entry = __builtin_amdgcn_s_memtime();
@@ -2274,9 +2366,10 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
                     }
                 }
             }
+            nst = -1;
             if (L > 0 && !(A.flags & kConeDiagNoMerge))
-                merge_levels<SMAX, RW>(C, buf, p, L, tid, st_regs, rs, o0, A.flags,
-                                       buf + kLdsBufFloats + 4 + (tid & 63), qout, begin_next);
+                nst = merge_levels<SMAX, RW>(C, buf, p, L, tid, st_regs, rs, o0, A.flags,
+                                             buf + kLdsBufFloats + 4 + (tid & 63), qout, begin_next);
             RT_MARK(3);
             // the output level: dense rows from the buffer start, or (no
             // merge level) the single bottom row where the DMA left it
@@ -2297,7 +2390,10 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
 #endif
             }
         }
-        if (!begun) begin_next();
+        if (!begun) {
+            begin_next();
+            nst = 0;
+        }
 #ifdef RT_STAMPS
         RT_MARK(4);
         tl[5] = t_entry;

@@ -9,6 +9,7 @@
 #   bash tools/gpu_run.sh TAG pmc [CFG]              PMC passes (4 counter groups) -> profiles/TAG_pmc_cone[_CFG].json
 #   bash tools/gpu_run.sh TAG configs [LIB...]       per-config table (tools/bench_configs.py) per library
 #   bash tools/gpu_run.sh TAG ab CFG LIB...          same-box A/B of builds: cone ms per trial, alternated twice
+#                                                    (AB_FLAGS=v1,v2: RIPTIDE_AMD_CONE_FLAGS values per build)
 #   bash tools/gpu_run.sh TAG flags CFG FLAGS...     same-box A/B of RIPTIDE_AMD_CONE_FLAGS values
 #   bash tools/gpu_run.sh TAG stamps CFG             per-phase stamps (libriptide_amd_stamps.so)
 #   bash tools/gpu_run.sh TAG trace LIB...           per-launch cone durations of the cfg2 bench per library
@@ -87,9 +88,9 @@ do_ab() {      # CFG LIB...
   for rep in 1 2; do
     for lib in "$@"; do
       local r
-      r=$(RIPTIDE_AMD_LIB=$lib timeout -k 10 200 python -u tools/ab_env.py RIPTIDE_AMD_CONE_FLAGS 7 "$cfg" 2>&1 | grep '"round": 1') \
+      r=$(RIPTIDE_AMD_LIB=$lib timeout -k 10 300 python -u tools/ab_env.py RIPTIDE_AMD_CONE_FLAGS "${AB_FLAGS:-7}" "$cfg" 2>&1 | grep '"round": 1') \
         || { echo "$lib failed"; exit 1; }
-      echo "$(basename "$lib") $r" | tee -a "$O/ab_$cfg.log"
+      echo "$r" | sed "s|^|$(basename "$lib") |" | tee -a "$O/ab_$cfg.log"
     done
   done
 }
@@ -118,9 +119,10 @@ do_trace() {
     (cd /tmp && export TMPDIR=/tmp && RIPTIDE_AMD_LIB=$R/$lib timeout -k 10 400 rocprofv3 --kernel-trace -d "$O/trace_$n" \
        -o run -f csv -- python3 "$R/bench.py" --no-cpu-baseline --steps 4 > "$O/trace_$n.log" 2>&1) \
       || fail "trace $n" "$O/trace_$n.log"
-    echo "== $n: $(tail -1 "$O/trace_$n.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["value"],2), "trials/s", d["config"]["cone_launches_per_step"], "launches", "checked", d.get("checked"))')"
+    grep '^{"metric"' "$O/trace_$n.log" > "$O/trace_$n.json" || fail "trace $n (no bench line)" "$O/trace_$n.log"
+    echo "== $n: $(python3 -c 'import json,sys; d=json.load(open(sys.argv[1])); print(round(d["value"],2), "trials/s", d["config"]["cone_launches_per_step"], "launches", "checked", d.get("checked"))' "$O/trace_$n.json")"
     python3 tools/prof_dispatch.py "$O/trace_$n" \
-      "$(tail -1 "$O/trace_$n.log" | python3 -c 'import json,sys; print(json.loads(sys.stdin.read())["config"]["cone_launches_per_step"])')" \
+      "$(python3 -c 'import json,sys; print(json.load(open(sys.argv[1]))["config"]["cone_launches_per_step"])' "$O/trace_$n.json")" 1 4 \
       | tee "$O/trace_$n.txt"
   done
 }

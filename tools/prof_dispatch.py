@@ -4,7 +4,9 @@ run (kernel_trace.csv): the cone dispatches in start order, grouped into
 steps of N launches (a bench step issues the same launch sequence every
 step), and the median duration of each launch position over the steps.
 
-usage: tools/prof_dispatch.py <dir with *kernel_trace.csv> N_LAUNCHES_PER_STEP
+usage: tools/prof_dispatch.py <dir with *kernel_trace.csv> N_LAUNCHES_PER_STEP [SKIP_STEPS [STEPS]]
+(bench.py: SKIP_STEPS = its warmup steps, STEPS = its timed steps; the
+self-check's default-schedule run that follows them is not counted)
 """
 import csv
 import glob
@@ -14,14 +16,17 @@ import sys
 
 def main():
     root, n = sys.argv[1], int(sys.argv[2])
+    skip = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+    want = int(sys.argv[4]) if len(sys.argv) > 4 else 0
     rows = []
     for f in glob.glob(root + "/**/*kernel_trace.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             if "cone_kernel" in r["Kernel_Name"]:
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
-    steps = len(rows) // n
-    rows = rows[len(rows) - steps * n:]          # whole steps, the last ones
+    rows = rows[skip * n:]
+    steps = len(rows) // n if not want else min(want, len(rows) // n)
+    rows = rows[:steps * n]
     print(f"{steps} steps x {n} cone launches")
     total = 0.0
     for i in range(n):
