@@ -218,7 +218,6 @@ enum : uint32_t {
     kConeStoreFromRegs = 1u,   // non-final passes store the output level straight from registers
     kConeFuse2 = 2u,           // two merge levels per LDS round trip where no level holds size-1 nodes
     kConeSnrStride = 4u,       // final passes keep their output rows at a bank-friendly stride for the S/N
-    kConePersist = 8u,         // persistent grid (two workgroups per CU), each starting its next unit itself
     kConeDiagNoSnr = 1u << 30, // diagnostics only (wrong results): skip the S/N epilogue
     kConeDiagNoMerge = 1u << 29, // diagnostics only (wrong results): skip the merge levels
     kConeDiagNoWrite = 1u << 28, // diagnostics only (wrong results): skip the level write-back

@@ -8,8 +8,6 @@
 // bit-identical to the strict restatement of downsample.hpp:44-82.
 #include <hip/hip_runtime.h>
 
-#include <algorithm>
-#include <utility>
 #include <cstdlib>
 
 #include "common.hpp"
@@ -373,51 +371,6 @@ __device__ __forceinline__ void dma_run(__amdgpu_buffer_rsrc_t rs, uint32_t goff
     }
 }
 
-// s_waitcnt vmcnt(n) for a wave-uniform n (the immediate of each case): the
-// wave's vector-memory operations other than its n youngest are done; n < 0
-// or beyond the counter's range waits for all of them.
-template <int N>
-__device__ __forceinline__ void wait_vmcnt_imm()
-{
-    __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 15) | ((N >> 4) << 14));
-}
-template <int... Ns>
-__device__ __forceinline__ void wait_vmcnt_sw(int n, std::integer_sequence<int, Ns...>)
-{
-    bool done = false;
-    ((n == Ns ? (wait_vmcnt_imm<Ns>(), done = true) : false), ...);
-    if (!done) wait_vmcnt_imm<0>();
-}
-__device__ __forceinline__ void wait_vmcnt_below(int n)
-{
-    wait_vmcnt_sw(uni(n), std::make_integer_sequence<int, 48>{});
-}
-
-// Exclusive prefix sum of v over the 64 lanes of a wave (DPP row shifts,
-// then the row broadcasts; bound_ctrl writes 0 where the source is outside).
-__device__ __forceinline__ int wave_excl_sum(int v, int lane)
-{
-    int x = v;
-    int y = __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);   // row_shr:1
-    x += (lane & 15) >= 1 ? y : 0;
-    y = __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);       // row_shr:2
-    x += (lane & 15) >= 2 ? y : 0;
-    y = __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);       // row_shr:4
-    x += (lane & 15) >= 4 ? y : 0;
-    y = __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);       // row_shr:8
-    x += (lane & 15) >= 8 ? y : 0;
-    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);     // row_bcast:15 -> rows 1, 3
-    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);     // row_bcast:31 -> rows 2, 3
-    return x - v;
-}
-
-// Tile units' bottom-level DMA derived from the unit record (1) or read from
-// the blob's host-built segment table (0: one more dependent memory round
-// trip at the unit's start).  A/B knob.
-#ifndef RT_ANALYTIC_FILL
-#define RT_ANALYTIC_FILL 1
-#endif
-
 // Starts unit (item, trial): its view, and (dma) the LDS DMA of its bottom
 // level into `buf` and, for a tile unit, of its blob into `aux`.  Nothing is
 // waited for: the caller waits (vmcnt) and barriers before reading LDS.
@@ -488,43 +441,7 @@ __device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t u, uin
 #ifdef RT_STAMPS
         if (ts) ts[1] = __builtin_amdgcn_s_memtime() + (ok ? 0 : 0);
 #endif
-        if (ok && dma && RT_ANALYTIC_FILL && C.tile) {
-            // the blob's LDS part: the last wave
-            const __amdgpu_buffer_rsrc_t rb = buffer_rsrc(a.blob + U.blob, (uint32_t)words * 4u);
-            if (wave == kConeWaves - 1) dma_run(rb, 0u, words >> 2, (float*)const_cast<uint32_t*>(C.aux), 0, 1, lane);
-            // the bottom level from the record alone: lane j < 2^L derives
-            // range j of the dependency cone (the split tree walked along the
-            // bits of j, head = 0, the planner's range order: build_tile_blob),
-            // its 16-byte-phase run and, by a wave prefix sum, its first LDS
-            // chunk; wave w then issues runs w, w + 8, ... in pieces of <= 64
-            // chunks -- no segment table and its memory round trip
-            const int L = U.levels;
-            uint32_t size = (uint32_t)U.node_size, lo = (uint32_t)U.s0, hi = (uint32_t)U.s1 - 1u,
-                     start = (uint32_t)U.node_start;
-            for (int l = L - 1; l >= 0; --l) {
-                const uint32_t bit = ((uint32_t)lane >> l) & 1u;
-                const uint32_t hs = size >> 1, cs = bit ? size - hs : hs;
-                const float k = merge_coef(cs, size);
-                lo = merge_index(k, lo);
-                hi = merge_index(k, hi);
-                start += bit ? hs : 0u;
-                size = cs;
-            }
-            const uint32_t first = (start + lo) * (uint32_t)p, al = first & 3u;
-            const int nch = lane < (1 << L) ? (int)(((hi - lo + 1u) * (uint32_t)p + al + 3u) >> 2) : 0;
-            const int g0 = (int)((first - al) >> 2);
-            const int cb = wave_excl_sum(nch, lane);
-            for (int j = wave; j < (1 << L); j += kConeWaves) {
-                const int c0 = __builtin_amdgcn_readlane(cb, j);
-                const int n = __builtin_amdgcn_readlane(nch, j);
-                const uint32_t g = (uint32_t)__builtin_amdgcn_readlane(g0, j);
-                for (int c = 0; c < n; c += 64)
-                    if (lane < n - c && 4 * (c0 + min(n, c + 64)) <= kLdsBufFloats && !(a.flags & kConeDiagNoFill))
-                        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                            rs, (__attribute__((address_space(3))) void*)(buf + 4 * (c0 + c)), 16,
-                            (int)((g + (uint32_t)(c + lane)) * 16u), 0, 0, kFillCpol);
-            }
-        } else if (ok && dma) {
+        if (ok && dma) {
             // DMA segments: wave w issues segments w, w + 8, ...; its lane i
             // holds segment w + 8i (one coalesced vector load)
             const uint4* const segs = reinterpret_cast<const uint4*>(a.blob + U.blob + words);
@@ -1164,13 +1081,11 @@ __device__ __forceinline__ void write_rows_slots(float* base, float* dummy, cons
     }
 }
 
-// Returns the wave's number of store instructions (uniform).
 template <int SMAX, int RW>
-__device__ __forceinline__ int store_rows_slots(const float (&v)[RW][SMAX], int p, int lane, uint32_t sw, int nq,
-                                                __amdgpu_buffer_rsrc_t rs, uint32_t st_o0)
+__device__ __forceinline__ void store_rows_slots(const float (&v)[RW][SMAX], int p, int lane, uint32_t sw, int nq,
+                                                 __amdgpu_buffer_rsrc_t rs, uint32_t st_o0)
 {
     const bool tail_ok = lane + 64 * (SMAX - 1) < p;
-    int n = 0;
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
         if (i / 2 < nq) {
@@ -1184,11 +1099,9 @@ __device__ __forceinline__ int store_rows_slots(const float (&v)[RW][SMAX], int 
                                                     : (tail_ok ? ob + 256u * (uint32_t)k : 0x80000000u);
                     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i][k]), rs, (int)o, 0, kStoreCpol);
                 }
-                n += SMAX;
             }
         }
     }
-    return n;
 }
 
 // kPack2 merge step (p <= 32; units always with a blob): register row i of
@@ -1438,19 +1351,16 @@ __device__ __forceinline__ void merge_step_tasks(const UnitCtx& C, const float* 
 // S/N identical.
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
-// Returns the wave's number of global store instructions (uniform).
 template <bool GLOBAL>
-__device__ __forceinline__ int put_tasks(float* base, int q, const float (&v)[kPackTasks][kPackSeg], int p, int tid,
-                                         int nrows, __amdgpu_buffer_rsrc_t rs, uint32_t st_o0)
+__device__ __forceinline__ void put_tasks(float* base, int q, const float (&v)[kPackTasks][kPackSeg], int p, int tid,
+                                          int nrows, __amdgpu_buffer_rsrc_t rs, uint32_t st_o0)
 {
     const int segs = pack_segments(p);
     const int ntask = nrows * segs;
     const int wave0 = tid & ~63;
-    int n = 0;
 #pragma unroll
     for (int i = 0; i < kPackTasks; ++i) {
         if (kConeBlock * i + wave0 < ntask) {
-            n += GLOBAL ? kPackSeg / 4 : 0;
             int r, j0;
             pack_task(min(tid + kConeBlock * i, ntask - 1), segs, p, r, j0);
             if constexpr (GLOBAL) {
@@ -1470,7 +1380,6 @@ __device__ __forceinline__ int put_tasks(float* base, int q, const float (&v)[kP
             }
         }
     }
-    return n;
 }
 
 // All merge levels of one unit, deepest first, in place in the dense rows
@@ -1479,12 +1388,10 @@ __device__ __forceinline__ int put_tasks(float* base, int q, const float (&v)[kP
 // Each level's outputs are staged in registers between two barriers, then
 // written back.  With `st` set (a non-final pass), the output level goes from
 // the staging registers straight to global memory instead of back into LDS.
-// Returns the wave's store instructions issued after pre_store() (a
-// non-final pass's output level from registers), or -1 if not counted.
-template <int SMAX, int RW, class PreStore>
-__device__ __forceinline__ int merge_levels(const UnitCtx& C, float* base, int p, int L, int tid, bool st,
+template <int SMAX, int RW>
+__device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int p, int L, int tid, bool st,
                                              __amdgpu_buffer_rsrc_t rs, uint32_t st_o0, uint32_t flags, float* dummy,
-                                             int qout, PreStore&& pre_store)
+                                             int qout)
 {
     const int lane = tid & 63, wave = tid >> 6;
     const bool tile = C.tile;
@@ -1518,14 +1425,14 @@ __device__ __forceinline__ int merge_levels(const UnitCtx& C, float* base, int p
                 }
                 l = lo - 1;
                 if (lo == 0 && st) {
-                    pre_store();
-                    return put_tasks<true>(base, qs, v, p, tid, nrows, rs, st_o0);
+                    put_tasks<true>(base, qs, v, p, tid, nrows, rs, st_o0);
+                    return;
                 }
                 if (!(flags & kConeDiagNoBarrier)) lds_barrier();
                 if (!(flags & kConeDiagNoWrite)) put_tasks<false>(base, qs, v, p, tid, nrows, rs, st_o0);
                 if (!(flags & kConeDiagNoBarrier)) lds_barrier();
             }
-            return -1;
+            return;
         }
         for (int l = L - 1; l >= 0;) {
             const bool two = fuse && l >= 1 && (tile || (node_size >> l) >= 2);
@@ -1544,15 +1451,14 @@ __device__ __forceinline__ int merge_levels(const UnitCtx& C, float* base, int p
             }
             l = lo - 1;
             if (lo == 0 && st) {
-                pre_store();
                 store_rows_lanes<RW>(v, p, lane, wave, nrows, rs, st_o0);
-                return -1;
+                return;
             }
             if (!(flags & kConeDiagNoBarrier)) lds_barrier();
             if (!(flags & kConeDiagNoWrite)) write_rows_lanes<RW>(base, dummy, v, p, lane, wave, nrows);
             if (!(flags & kConeDiagNoBarrier)) lds_barrier();
         }
-        return -1;
+        return;
     }
     if constexpr (SMAX <= 5) {
         if (C.slots && fuse) {
@@ -1570,8 +1476,8 @@ __device__ __forceinline__ int merge_levels(const UnitCtx& C, float* base, int p
                 else merge_step_slots<SMAX, RW, false>(C, src, p, lo, lane, wave, v, lo_src, sw, nq);
                 l = lo - 1;
                 if (lo == 0 && st) {
-                    pre_store();
-                    return store_rows_slots<SMAX, RW>(v, p, lane, sw, nq, rs, st_o0);
+                    store_rows_slots<SMAX, RW>(v, p, lane, sw, nq, rs, st_o0);
+                    return;
                 }
                 if (!(flags & kConeDiagNoBarrier)) lds_barrier();
                 // the output level of a final pass at row stride qout (the S/N's)
@@ -1579,7 +1485,7 @@ __device__ __forceinline__ int merge_levels(const UnitCtx& C, float* base, int p
                     write_rows_slots<SMAX, RW>(base, dummy, v, p, lane, sw, nq, lo == 0 ? qout : p);
                 if (!(flags & kConeDiagNoBarrier)) lds_barrier();
             }
-            return -1;
+            return;
         }
     }
     for (int l = L - 1; l >= 0;) {
@@ -1602,9 +1508,8 @@ __device__ __forceinline__ int merge_levels(const UnitCtx& C, float* base, int p
             merge_level_dense<S, RW, false>(C, src, p, l, lane, wave, nr, v, lo_src);
         l = lo - 1;
         if (lo == 0 && st) {
-            pre_store();
             store_rows<S, RW>(v, p, lane, wave, nr, rs, st_o0);
-            return -1;
+            return;
         }
         if (!(flags & kConeDiagNoBarrier)) lds_barrier();
         if (!(flags & kConeDiagNoWrite)) {
@@ -1612,7 +1517,6 @@ __device__ __forceinline__ int merge_levels(const UnitCtx& C, float* base, int p
         }
         if (!(flags & kConeDiagNoBarrier)) lds_barrier();
     }
-    return -1;
 }
 
 template <int CTRL>
@@ -2213,17 +2117,11 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
 #endif
 
 // One kernel per merge slot width SMAX (units with ceil(p/64) <= SMAX), so each
-// gets its own register allocation.  Two workgroups per CU; workgroup b runs
-// units u = b, b + G, b + 2G, ... (G = gridDim.x; unit u = item u / batch,
-// trial u % batch; items are sorted longest first, so every workgroup's
-// share is alike).  With G = the number of units (one unit per workgroup) the
-// hardware dispatcher starts each unit; with a persistent grid (2 per CU,
-// kConePersist) a workgroup starts its next unit itself, as soon as the
-// current one no longer reads its LDS level buffer: a merge-only unit
-// stores its output level straight from registers, so the next unit's
-// record, DMA segments and bottom-level fill are issued just before that
-// store and land while it drains.
-//   begin(u) | wait | merge(u) .. last step | begin(u + G) | store(u) | wait | merge(u + G) ..
+// gets its own register allocation; one workgroup per unit u = blockIdx.x
+// (unit u = item u / batch, trial u % batch; items are sorted longest first),
+// two workgroups per CU: a unit's DMA is waited for at its start, the CU's
+// other workgroup filling the wait.
+//   begin(u) [DMA] | wait | merge(u) | store or S/N(u)
 // SNR: the launch's units all end in the fused S/N (final passes) -- or none
 // does (the merge-only passes store their output level): separate instances,
 // so a merge-only launch carries no S/N code and no S/N register floor.
@@ -2243,189 +2141,143 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
 
     const int tid = threadIdx.x;
 #ifdef RT_STAMPS
-    unsigned long long t_entry = __builtin_amdgcn_s_memtime();
-    unsigned long long r_entry = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long t_entry = __builtin_amdgcn_s_memtime();
+    const unsigned long long r_entry = __builtin_amdgcn_s_memrealtime();
     unsigned long long t_begin[3] = {};
 #endif
     const uint32_t total = a.num_items * a.batch;
-    uint32_t u = blockIdx.x;
-    if (u >= total) return;
+    if (blockIdx.x >= total) return;
+    const uint32_t u = blockIdx.x;
     if (tid < (int)a.num_widths) wl[tid] = (int)a.widths[tid];   // visible after the first barrier
     if (tid == 0) {
         uint32_t wm = 0;
         for (uint32_t i = 0; i < a.num_widths; ++i) wm = max(wm, a.widths[i]);
         wl[kMaxWidths] = (int)wm;
     }
+    const bool dma = !(a.flags & kConeDiagNoLand);
+    bool ok;
+#ifdef RT_STAMPS
+    const UnitCtx C = unit_begin<SMAX, RW>(a, u, aux, data, tid, dma, ok, t_begin);
+    unsigned long long tl[kStampMarks] = {};
+    tl[0] = __builtin_amdgcn_s_memtime();
+#else
+    const UnitCtx C = unit_begin<SMAX, RW>(a, u, aux, data, tid, dma, ok);
+#endif
+    const UnitView& U = C.U;
+    const int p = U.p;
+    const int L = U.levels;
     float* const buf = data;
-    // the launch's arguments re-read (scalar loads from the kernarg segment)
-    // in every unit, through a pointer the compiler cannot see is invariant:
-    // nothing per launch or per unit is hoisted out of the unit loop into
-    // long-lived (spilled) SGPRs.  Only u is carried from one unit to the next.
-    typedef const __attribute__((address_space(4))) ConeArgs* kargs_ptr;
-    const kargs_ptr kp = (kargs_ptr)__builtin_amdgcn_kernarg_segment_ptr();
-    bool first = true;
-    int nst = 0;    // the wave's stores issued after the current unit's DMA (-1: not counted)
-    for (;;) {
-        kargs_ptr kpl = kp;
-        asm volatile("" : "+s"(kpl));
-        const ConeArgs& A = *(const ConeArgs*)kpl;
-        const bool dma = !(A.flags & kConeDiagNoLand);
-        bool ok;
-        // the first unit's DMA is issued here; every later unit's was issued
-        // by begin_next of the unit before (this call re-reads its record)
-#ifdef RT_STAMPS
-        UnitCtx C = unit_begin<SMAX, RW>(A, u, aux, data, tid, dma && first, ok, first ? t_begin : nullptr);
-        unsigned long long tl[kStampMarks] = {};
-        tl[0] = __builtin_amdgcn_s_memtime();
-#else
-        UnitCtx C = unit_begin<SMAX, RW>(A, u, aux, data, tid, dma && first, ok);
-#endif
-        first = false;
-        const UnitView& U = C.U;
-        const int p = U.p;
-        const int L = U.levels;
-        // the launch kind is the unit's (the planner splits final and merge-
-        // only launches; validate_exec_plan)
-        ok = ok && ((U.dst == kSelSnr) == SNR);
-        // a final pass's per-width S/N constants, published by the barrier
-        // below (the S/N row passes have no barrier of their own)
-        if (SNR && tid < (int)A.num_widths) snr_width_consts(wl[tid], p, whb + 2 * tid);
-        // the roll table of a 4-slot unit (past its blob's LDS part, which
-        // the DMA may still be writing), published by the barrier below
-        if constexpr (SMAX == 4)
-            if (C.slots && ok) build_roll_lut4(aux + kLut4Off, p, tid);
-        // the short-row roll table in the unused metadata area
+    // the launch kind is the unit's (the planner splits final and merge-only
+    // launches; validate_exec_plan)
+    ok = ok && ((U.dst == kSelSnr) == SNR);
+    // a final pass's per-width S/N constants, published by the barrier below
+    // (the S/N row passes have no barrier of their own)
+    if (SNR && tid < (int)a.num_widths) snr_width_consts(wl[tid], p, whb + 2 * tid);
+    // the roll table of a 4-slot unit (past its blob's LDS part, which the
+    // DMA may still be writing), published by the barrier below
+    if constexpr (SMAX == 4)
+        if (C.slots && ok) build_roll_lut4(aux + kLut4Off, p, tid);
+    // the short-row roll table in the unused metadata area
+    if constexpr (SMAX == kPack2)
+        if (ok && p >= kPackSeg) build_pack_lut(aux, p, tid);
+    // every wave waits for its own DMA, the barrier publishes all of them
+    __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)
+    lds_barrier();
+    RT_MARK(1);
+    RT_MARK(2);
+    if (!ok) {
+        if (tid == 0 && a.error_flag) atomicOr(a.error_flag, 1);
+    } else {
+        // merge levels, deepest first; a non-final pass stores its output
+        // level straight from registers (st), a final pass keeps it in LDS
+        // for the S/N epilogue
+        constexpr bool st = !SNR;
+        const bool st_regs = st && (a.flags & kConeStoreFromRegs);
+        const float* dst = (U.dst == kSelPing ? a.ping : a.pong) + (uint64_t)U.trial * a.buf_stride + U.buf_off;
+        const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(dst, (((uint32_t)U.m * (uint32_t)p + 3u) & ~3u) * 4u);
+        const uint32_t o0 = (uint32_t)(U.node_start + U.s0) * (uint32_t)p * 4u;
+        const int n0 = rows_at(C, 0);
+        // a final pass's output level at a row stride = 16 (mod 32): the
+        // S/N epilogue's lane groups (two rows of 16 lanes per 32-lane LDS
+        // group, odd chunk strides) then read and write on distinct banks
+        // (at stride p they collided on up to 10 of 32 banks)
+        int qout = p;
+        // short rows in (row, segment) tasks: every level above the fill at
+        // the odd stride pack_stride(p)
         if constexpr (SMAX == kPack2)
-            if (ok && p >= kPackSeg) build_pack_lut(aux, p, tid);
-        // every wave waits for its own DMA, the barrier publishes all of it;
-        // the previous unit's stores, issued after this unit's DMA and counted
-        // in the same in-order counter, may stay in flight (vmcnt(nst))
-        wait_vmcnt_below(nst);
-        lds_barrier();
-        RT_MARK(1);
-        RT_MARK(2);
-        // the next unit of this workgroup: begun (record, DMA segments, fill
-        // and blob DMA into the level buffer) once every wave is past its
-        // last LDS read of this unit
-        // (final units run one per workgroup: their S/N reads the level
-        // buffer to the end, so the next unit could start only after it)
-        const uint32_t un = u + gridDim.x;
-        const bool has_next = !SNR && un < total;
-        bool begun = false;
-        auto begin_next = [&]() {
-            if (has_next) {
-                lds_barrier();                // the level buffer and metadata area are free
-                bool ok_next;
-#ifdef RT_STAMPS
-                t_entry = __builtin_amdgcn_s_memtime();
-                (void)unit_begin<SMAX, RW>(A, un, aux, data, tid, dma, ok_next, t_begin);
-#else
-                (void)unit_begin<SMAX, RW>(A, un, aux, data, tid, dma, ok_next);
-#endif
-            }
-            begun = true;
-        };
-        if (!ok) {
-            if (tid == 0 && A.error_flag) atomicOr(A.error_flag, 1);
-        } else {
-            // merge levels, deepest first; a non-final pass stores its output
-            // level straight from registers (st), a final pass keeps it in LDS
-            // for the S/N epilogue
-            constexpr bool st = !SNR;
-            const bool st_regs = st && (A.flags & kConeStoreFromRegs);
-            const float* dst = (U.dst == kSelPing ? A.ping : A.pong) + (uint64_t)U.trial * A.buf_stride + U.buf_off;
-            const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(dst, (((uint32_t)U.m * (uint32_t)p + 3u) & ~3u) * 4u);
-            const uint32_t o0 = (uint32_t)(U.node_start + U.s0) * (uint32_t)p * 4u;
-            const int n0 = rows_at(C, 0);
-            // a final pass's output level at a row stride = 16 (mod 32): the
-            // S/N epilogue's lane groups (two rows of 16 lanes per 32-lane LDS
-            // group, odd chunk strides) then read and write on distinct banks
-            // (at stride p they collided on up to 10 of 32 banks)
-            int qout = p;
-            // short rows in (row, segment) tasks: every level above the fill
-            // at the odd stride pack_stride(p)
-            if constexpr (SMAX == kPack2)
-                if (L > 0) qout = pack_stride(p);
-            if constexpr (SMAX <= 5 && SMAX != kPack2) {
-                // = 16 (mod 32) and >= p + kSnrMaxChunk (room for the S/N's
-                // whole-chunk prefix writes and its wrapped prefix extension),
-                // else >= p + kSnrWin (the extension only)
-                const int qa = p + kSnrMaxChunk + ((16 - ((p + kSnrMaxChunk) & 31)) & 31);
-                const int qb = p + kSnrWin + ((16 - ((p + kSnrWin) & 31)) & 31);
-                if (!st && L > 0 && C.slots && (A.flags & kConeFuse2) && (A.flags & kConeSnrStride)) {
-                    qout = n0 * qa <= kLdsDataFloats ? qa : (n0 * qb <= kLdsDataFloats ? qb : p);
-                    // widths past the register window: a stride with room for
-                    // their plain-LDS windows (snr_wide_stride), = 16 (mod 32)
-                    // where that fits too
-                    const int wmax = wl[kMaxWidths];
-                    if (WIDE && snr_group(p) == 16 && wmax > kSnrWin && wmax < p) {
-                        const int qw = snr_wide_stride(p, wmax);
-                        const int qwp = qw + ((16 - (qw & 31)) & 31);
-                        if (n0 * qwp <= kLdsDataFloats) qout = qwp;
-                        else if (n0 * qw <= kLdsDataFloats) qout = qw;
-                    }
+            if (L > 0) qout = pack_stride(p);
+        if constexpr (SMAX <= 5 && SMAX != kPack2) {
+            // = 16 (mod 32) and >= p + kSnrMaxChunk (room for the S/N's whole-
+            // chunk prefix writes and its wrapped prefix extension), else >=
+            // p + kSnrWin (the extension only)
+            const int qa = p + kSnrMaxChunk + ((16 - ((p + kSnrMaxChunk) & 31)) & 31);
+            const int qb = p + kSnrWin + ((16 - ((p + kSnrWin) & 31)) & 31);
+            if (!st && L > 0 && C.slots && (a.flags & kConeFuse2) && (a.flags & kConeSnrStride)) {
+                qout = n0 * qa <= kLdsDataFloats ? qa : (n0 * qb <= kLdsDataFloats ? qb : p);
+                // widths past the register window: a stride with room for
+                // their plain-LDS windows (snr_wide_stride), = 16 (mod 32)
+                // where that fits too
+                const int wmax = wl[kMaxWidths];
+                if (WIDE && snr_group(p) == 16 && wmax > kSnrWin && wmax < p) {
+                    const int qw = snr_wide_stride(p, wmax);
+                    const int qwp = qw + ((16 - (qw & 31)) & 31);
+                    if (n0 * qwp <= kLdsDataFloats) qout = qwp;
+                    else if (n0 * qw <= kLdsDataFloats) qout = qw;
                 }
             }
-            nst = -1;
-            if (L > 0 && !(A.flags & kConeDiagNoMerge))
-                nst = merge_levels<SMAX, RW>(C, buf, p, L, tid, st_regs, rs, o0, A.flags,
-                                             buf + kLdsBufFloats + 4 + (tid & 63), qout, begin_next);
-            RT_MARK(3);
-            // the output level: dense rows from the buffer start, or (no
-            // merge level) the single bottom row where the DMA left it
-            float* const obase = L > 0 ? buf : buf + (C.table ? uni(bottom_offsets(C)[0]) : C.al);
-            if (st) {
-                if (!begun) {
-                    const int qst = L > 0 ? qout : p;    // the merged level's LDS row stride
-                    for (int r = 0; r < n0; ++r)
-                        for (int j = tid; j < p; j += kConeBlock)
-                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(obase[r * qst + j]), rs,
-                                                                  (int)(o0 + (uint32_t)(r * p + j) * 4u), 0, kStoreCpol);
-                }
-            } else if constexpr (SNR) {
-#ifdef RT_STAMPS
-                if (!(A.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(A, U, obase, qout, wl, n0, tid, whb, tl);
-#else
-                if (!(A.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(A, U, obase, qout, wl, n0, tid, whb, nullptr);
-#endif
+        }
+        if (L > 0 && !(a.flags & kConeDiagNoMerge))
+            merge_levels<SMAX, RW>(C, buf, p, L, tid, st_regs, rs, o0, a.flags, buf + kLdsBufFloats + 4 + (tid & 63),
+                                   qout);
+        RT_MARK(3);
+        // the output level: dense rows from the buffer start, or (no merge
+        // level) the single bottom row where the DMA left it
+        float* const obase = L > 0 ? buf : buf + (C.table ? uni(bottom_offsets(C)[0]) : C.al);
+        if (st) {
+            if (L == 0 || !st_regs) {
+                const int qst = L > 0 ? qout : p;    // the merged level's LDS row stride
+                for (int r = 0; r < n0; ++r)
+                    for (int j = tid; j < p; j += kConeBlock)
+                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(obase[r * qst + j]), rs,
+                                                              (int)(o0 + (uint32_t)(r * p + j) * 4u), 0, kStoreCpol);
             }
-        }
-        if (!begun) {
-            begin_next();
-            nst = 0;
-        }
+        } else if constexpr (SNR) {
 #ifdef RT_STAMPS
-        RT_MARK(4);
-        tl[5] = t_entry;
-        tl[11] = t_begin[0];
-        tl[12] = t_begin[1];
-        tl[13] = t_begin[2];
-        RT_MARK(6);
-        tl[14] = r_entry;
-        tl[15] = __builtin_amdgcn_s_memrealtime();
-        r_entry = tl[15];
-        if (tid == 0 && A.stamps) {
-            unsigned long long* e = A.stamps + (uint64_t)kStampRecWords * (uint64_t)u;
-            const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));     // HW_REG_HW_ID
-            const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11));   // HW_REG_XCC_ID
-            e[0] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
-#pragma unroll
-            for (int i = 0; i < kStampMarks; ++i) e[1 + i] = tl[i];
-            e[1 + kStampMarks] = (unsigned long long)p | ((unsigned long long)L << 16) |
-                                 ((unsigned long long)U.mode << 24) | ((unsigned long long)rows_at(C, 0) << 32) |
-                                 ((unsigned long long)(U.dst == kSelSnr) << 48);
-        }
+            if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(a, U, obase, qout, wl, n0, tid, whb, tl);
+#else
+            if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(a, U, obase, qout, wl, n0, tid, whb, nullptr);
 #endif
-        if (!has_next) break;
-        u = un;
+        }
     }
-    // the last unit's global stores need no wait before the end of the
-    // program; every DMA was waited for at its unit's start
+#ifdef RT_STAMPS
+    lds_barrier();
+    RT_MARK(4);
+    tl[5] = t_entry;
+    tl[11] = t_begin[0];
+    tl[12] = t_begin[1];
+    tl[13] = t_begin[2];
+    RT_MARK(6);
+    tl[14] = r_entry;
+    tl[15] = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0 && a.stamps) {
+        unsigned long long* e = a.stamps + (uint64_t)kStampRecWords * (uint64_t)u;
+        const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));     // HW_REG_HW_ID
+        const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11));   // HW_REG_XCC_ID
+        e[0] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+#pragma unroll
+        for (int i = 0; i < kStampMarks; ++i) e[1 + i] = tl[i];
+        e[1 + kStampMarks] = (unsigned long long)p | ((unsigned long long)L << 16) |
+                             ((unsigned long long)U.mode << 24) | ((unsigned long long)rows_at(C, 0) << 32) |
+                             ((unsigned long long)(U.dst == kSelSnr) << 48);
+    }
+#endif
+    // every DMA was waited for at the unit start, and the unit's global
+    // stores need no wait before the end of the program
 }
 
-// Grid: one workgroup per unit, or (kConePersist, merge-only launches) a
-// persistent grid of two workgroups per CU that start their next unit
-// themselves (cone_kernel).
+// One workgroup per unit: the hardware dispatcher keeps both of a CU's
+// workgroup slots busy to the end of the launch (measured: 10.37 vs 11.55 ms
+// per cfg2 trial against a persistent grid, round 1).
 template <int SMAX, int RW = 0>
 static hipError_t launch_kind(const ConeArgs& args, dim3 g, dim3 b, bool wide_snr, bool snr, hipStream_t s)
 {
@@ -2447,13 +2299,7 @@ hipError_t launch_cone(const ConeArgs& args, uint32_t smax, uint32_t rw, bool wi
     if (!args.num_items || !args.batch) return hipSuccess;
     const uint64_t total = (uint64_t)args.num_items * args.batch;
     if (total > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    uint64_t grid = total;
-    if ((args.flags & kConePersist) && !snr) {
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        grid = std::min<uint64_t>(total, (uint64_t)cus * kConeWgsPerCu);
-    }
-    const dim3 g((uint32_t)grid), b(kConeBlock);
+    const dim3 g((uint32_t)total), b(kConeBlock);
     hipError_t e = hipErrorInvalidValue;
     switch (smax) {
     case 1:

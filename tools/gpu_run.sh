@@ -14,6 +14,8 @@
 #   bash tools/gpu_run.sh TAG stamps CFG             per-phase stamps (libriptide_amd_stamps.so)
 #   bash tools/gpu_run.sh TAG trace LIB...           per-launch cone durations of the cfg2 bench per library
 #   bash tools/gpu_run.sh TAG parity LIB...          GPU parity tests (test_gpu_parity.py) per library
+#   bash tools/gpu_run.sh TAG pmcflags CFG FLAGS...  instruction counters per RIPTIDE_AMD_CONE_FLAGS value
+#                                                    (diagnostic bits: phase attribution of VALU / SALU / LDS)
 #   bash tools/gpu_run.sh TAG round                  round-end pass: pmc (cfg2, cfg3), tests, smoke,
 #                                                    bench cfg2 / cfg3 / cfg5, configs, prof
 set -o pipefail
@@ -46,7 +48,7 @@ do_bench() {   # $1: log name, rest: bench.py arguments
 
 do_prof() {
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -f csv \
-     -- python3 "$R/bench.py" --no-cpu-baseline > "$O/bench_prof.log" 2>&1) || fail rocprof "$O/bench_prof.log"
+     -- python3 "$R/bench.py" --no-cpu-baseline --no-self-check > "$O/bench_prof.log" 2>&1) || fail rocprof "$O/bench_prof.log"
   tail -1 "$O/bench_prof.log" | cut -c1-300
   find "$O/prof" -name '*stats*'
 }
@@ -58,7 +60,7 @@ do_pmc() {     # $1: cfg2 (bench.py, 2 trials) or a config name (tools/ab_flags.
     i=$((i+1))
     if [ "$cfg" = cfg2 ]; then
       (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace -f csv -d "$d/p$i" -o run \
-         -- python3 "$R/bench.py" --steps 1 --warmup 1 --batch 2 --no-cpu-baseline > "$d/p$i.log" 2>&1) \
+         -- python3 "$R/bench.py" --steps 1 --warmup 1 --batch 2 --no-cpu-baseline --no-self-check > "$d/p$i.log" 2>&1) \
         || fail "pmc pass $i" "$d/p$i.log"
     else
       (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace -f csv -d "$d/p$i" -o run \
@@ -136,6 +138,33 @@ do_parity() {
   done
 }
 
+do_pmcflags() {   # CFG FLAGS...
+  local cfg=$1; shift
+  for f in "$@"; do
+    local d="$O/pmcflags_${cfg}_$f"
+    (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS \
+       SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE GRBM_COUNT \
+       --kernel-trace -f csv -d "$d" -o run -- python3 "$R/tools/ab_flags.py" "$f" "$cfg" > "$d.log" 2>&1) \
+      || fail "pmcflags $f" "$d.log"
+    python3 - "$d" "$f" <<'PY'
+import csv, glob, sys
+from collections import defaultdict
+S = defaultdict(float); t = 0.0
+for fn in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(fn)):
+        if "cone_kernel" in r.get("Kernel_Name", ""):
+            S[r["Counter_Name"]] += float(r["Counter_Value"])
+for fn in glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True):
+    for r in csv.DictReader(open(fn)):
+        if "cone_kernel" in r["Kernel_Name"]:
+            t += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+tr = 64.0
+print("flags", sys.argv[2], "per trial:", {k: "%.4g" % (v / tr) for k, v in sorted(S.items())},
+      "cone_ms_per_trial %.4f" % (t / tr * 1e3), "clock_GHz %.3f" % (S["GRBM_GUI_ACTIVE"] / 8 / t / 1e9 if t else 0))
+PY
+  done
+}
+
 case "$CMD" in
   tests) do_tests ;;
   bench) do_bench bench "$@" ;;
@@ -147,6 +176,7 @@ case "$CMD" in
   stamps) do_stamps "$@" ;;
   trace) do_trace "$@" ;;
   parity) do_parity "$@" ;;
+  pmcflags) do_pmcflags "$@" ;;
   round)
     do_pmc cfg2
     do_pmc cfg3
