@@ -130,6 +130,14 @@ uint64_t scratch_budget_floats()
     return 96ull << 20;   // 384 MiB per ping/pong buffer and trial: ~94 launches per cfg2 plan (sweep_schedule.py)
 }
 
+// Scratch banks of a periodogram plan: 2 (RIPTIDE_AMD_COSCHED=1) runs its
+// transform groups co-scheduled on two streams (run_cone_launches)
+uint32_t cosched_banks()
+{
+    const char* e = std::getenv("RIPTIDE_AMD_COSCHED");
+    return e && e[0] == '1' ? 2u : 1u;
+}
+
 // ---- profiling of cone / downsample launches
 struct ProfRec {
     hipEvent_t a, b;
@@ -162,15 +170,53 @@ std::atomic<int> g_test_corrupt{0};
 #endif
 
 // ---- a compiled plan resident on one device
+// A side stream and events for co-scheduled pass sequences (run_cone_launches),
+// taken by one call at a time from the plan's pool.
+struct SideSet {
+    hipStream_t s2 = nullptr;
+    std::vector<hipEvent_t> ev;
+};
+
 struct DevicePlan {
     ExecPlan ex;
     UnitDesc* d_units = nullptr;
     uint32_t* d_blob = nullptr;     // tile-unit metadata (build_tile_blob)
     int device = 0;
+    mutable std::mutex side_mu;
+    mutable std::vector<std::unique_ptr<SideSet>> side_all;
+    mutable std::vector<SideSet*> side_free;
     ~DevicePlan()
     {
         if (d_units) (void)hipFree(d_units);
         if (d_blob) (void)hipFree(d_blob);
+        for (auto& ss : side_all) {
+            for (hipEvent_t e : ss->ev) (void)hipEventDestroy(e);
+            if (ss->s2) (void)hipStreamDestroy(ss->s2);
+        }
+    }
+    SideSet* take_side(size_t events) const
+    {
+        std::lock_guard<std::mutex> lk(side_mu);
+        SideSet* ss;
+        if (!side_free.empty()) {
+            ss = side_free.back();
+            side_free.pop_back();
+        } else {
+            side_all.push_back(std::make_unique<SideSet>());
+            ss = side_all.back().get();
+            ck(hipStreamCreateWithFlags(&ss->s2, hipStreamNonBlocking), "hipStreamCreate");
+        }
+        while (ss->ev.size() < events) {
+            hipEvent_t e;
+            ck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+            ss->ev.push_back(e);
+        }
+        return ss;
+    }
+    void give_side(SideSet* ss) const
+    {
+        std::lock_guard<std::mutex> lk(side_mu);
+        side_free.push_back(ss);
     }
     void upload()
     {
@@ -235,46 +281,97 @@ uint64_t g_stamp_units = 0;      // unit records written since the last reset
 std::vector<uint64_t> g_stamp_launch;   // first record of each launch since the last reset
 
 // Run all cone launches of an exec plan.
+// One cone launch of a plan on stream s (profiling: HIP events around it
+// unless `prof_each` is off).
+void cone_launch(const DevicePlan& P, const Launch& L, ConeArgs a, uint32_t batch, hipStream_t s, bool prof_each)
+{
+    a.items = P.d_units + L.first;
+    a.num_items = L.count;
+    const uint64_t units = (uint64_t)L.count * batch;   // one workgroup per (item, trial)
+    if (L.count > 0x7FFFFFFFu || batch > 65535u) throw std::invalid_argument("too many cone work units in one launch");
+    // diagnostic builds: this launch's unit records follow the previous ones
+    a.stamps = nullptr;
+    if (g_stamps) {
+        std::lock_guard<std::mutex> lk(g_prof.mu);
+        if (g_stamp_units + units <= kTimelineCap) {
+            a.stamps = g_stamps + g_stamp_units * kStampRecWords;
+            g_stamp_launch.push_back(g_stamp_units);
+            g_stamp_units += units;
+        }
+    }
+    ProfRec r{};
+    const bool prof = g_prof.on && prof_each;
+    if (prof) {
+        {
+            std::lock_guard<std::mutex> lk(g_prof.mu);
+            r.a = g_prof.ev();
+            r.b = g_prof.ev();
+        }
+        r.alg = L.alg_bytes * batch;
+        r.moved = L.moved_bytes * batch;
+        ck(hipEventRecord(r.a, s), "hipEventRecord");
+    }
+    ck(launch_cone(a, L.smax, L.rw, L.wide_snr != 0, L.snr != 0, s), "cone_kernel");
+    if (prof) {
+        ck(hipEventRecord(r.b, s), "hipEventRecord");
+        std::lock_guard<std::mutex> lk(g_prof.mu);
+        g_prof.rec[0].push_back(r);
+    }
+}
+
+// Run all cone launches of an exec plan.  A plan with two scratch banks
+// (ExecPlan::banks) runs its transform groups co-scheduled on two streams:
+// group g on stream g mod 2, its merge-only launches starting once group g - 1
+// has finished its own merge-only launches -- so group g's merge-only passes
+// (latency / LDS bound) share the CUs with group g - 1's final passes (VALU
+// bound: the fused S/N).  Profiling then records one event pair around the
+// whole sequence (launches overlap) with their summed algorithmic bytes.
 void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStream_t s)
 {
     a.batch = batch;
     a.flags = kConeDefaultFeatures;
     if (const char* e = std::getenv("RIPTIDE_AMD_CONE_FLAGS")) a.flags = (uint32_t)std::strtoul(e, nullptr, 0);
     a.blob = P.d_blob;
-    for (size_t li = 0; li < P.ex.launches.size(); ++li) {
-        const Launch& L = P.ex.launches[li];
-        a.items = P.d_units + L.first;
-        a.num_items = L.count;
-        const uint64_t units = (uint64_t)L.count * batch;   // one workgroup per (item, trial)
-        if (L.count > 0x7FFFFFFFu || batch > 65535u) throw std::invalid_argument("too many cone work units in one launch");
-        // diagnostic builds: this launch's unit records follow the previous ones
-        a.stamps = nullptr;
-        if (g_stamps) {
+    const std::vector<Launch>& Ls = P.ex.launches;
+    if (P.ex.banks < 2 || P.ex.groups < 2) {
+        for (const Launch& L : Ls) cone_launch(P, L, a, batch, s, true);
+        return;
+    }
+    const uint32_t G = P.ex.groups;
+    SideSet* ss = P.take_side(2 + G);
+    ProfRec r{};
+    const bool prof = g_prof.on;
+    if (prof) {
+        {
             std::lock_guard<std::mutex> lk(g_prof.mu);
-            if (g_stamp_units + units <= kTimelineCap) {
-                a.stamps = g_stamps + g_stamp_units * kStampRecWords;
-                g_stamp_launch.push_back(g_stamp_units);
-                g_stamp_units += units;
-            }
+            r.a = g_prof.ev();
+            r.b = g_prof.ev();
         }
-        ProfRec r{};
-        const bool prof = g_prof.on;
-        if (prof) {
-            {
-                std::lock_guard<std::mutex> lk(g_prof.mu);
-                r.a = g_prof.ev();
-                r.b = g_prof.ev();
-            }
-            r.alg = L.alg_bytes * batch;
-            r.moved = L.moved_bytes * batch;
-            ck(hipEventRecord(r.a, s), "hipEventRecord");
+        for (const Launch& L : Ls) {
+            r.alg += L.alg_bytes * batch;
+            r.moved += L.moved_bytes * batch;
         }
-        ck(launch_cone(a, L.smax, L.rw, L.wide_snr != 0, L.snr != 0, s), "cone_kernel");
-        if (prof) {
-            ck(hipEventRecord(r.b, s), "hipEventRecord");
-            std::lock_guard<std::mutex> lk(g_prof.mu);
-            g_prof.rec[0].push_back(r);
-        }
+        ck(hipEventRecord(r.a, s), "hipEventRecord");
+    }
+    hipEvent_t fork = ss->ev[0], join = ss->ev[1];
+    ck(hipEventRecord(fork, s), "hipEventRecord");
+    ck(hipStreamWaitEvent(ss->s2, fork, 0), "hipStreamWaitEvent");
+    size_t li = 0;
+    for (uint32_t g = 0; g < G; ++g) {
+        hipStream_t st = (g & 1u) ? ss->s2 : s;
+        if (g >= 1) ck(hipStreamWaitEvent(st, ss->ev[2 + g - 1], 0), "hipStreamWaitEvent");
+        while (li < Ls.size() && Ls[li].group == g && !Ls[li].snr) cone_launch(P, Ls[li++], a, batch, st, false);
+        ck(hipEventRecord(ss->ev[2 + g], st), "hipEventRecord");
+        while (li < Ls.size() && Ls[li].group == g) cone_launch(P, Ls[li++], a, batch, st, false);
+    }
+    if (li != Ls.size()) throw std::runtime_error("cone launches out of group order");
+    ck(hipEventRecord(join, ss->s2), "hipEventRecord");
+    ck(hipStreamWaitEvent(s, join, 0), "hipStreamWaitEvent");
+    P.give_side(ss);
+    if (prof) {
+        ck(hipEventRecord(r.b, s), "hipEventRecord");
+        std::lock_guard<std::mutex> lk(g_prof.mu);
+        g_prof.rec[0].push_back(r);
     }
 }
 
@@ -441,7 +538,7 @@ rt_plan* make_plan(size_t size, double tsamp, const uint64_t* widths, size_t nw,
         }
         // scratch budget per ping/pong buffer and trial (scratch_budget_floats)
         const uint32_t wmax = P->widths.empty() ? 0u : *std::max_element(P->widths.begin(), P->widths.end());
-        build_exec_plan(xf, true, (uint32_t)nw, scratch_budget_floats(), P->dp.ex, wmax);
+        build_exec_plan(xf, true, (uint32_t)nw, scratch_budget_floats(), P->dp.ex, wmax, cosched_banks());
         P->dp.upload();
         ck(hipMalloc(&P->d_flag, sizeof(int)), "hipMalloc");
         ck(hipMemset(P->d_flag, 0, sizeof(int)), "hipMemset");
@@ -1028,7 +1125,7 @@ int rt_schedule_check(size_t size, double tsamp, size_t nw, double pmin, double 
         ExecPlan ex;
         // build_exec_plan validates the schedule (validate_exec_plan: tiles
         // inside nodes, LDS / register budgets, final pass covers every row)
-        build_exec_plan(xf, true, (uint32_t)nw, scratch_budget_floats(), ex);
+        build_exec_plan(xf, true, (uint32_t)nw, scratch_budget_floats(), ex, 0, cosched_banks());
         uint64_t a = 0;
         double alg = 0, mv = 0;
         for (const Launch& L : ex.launches) {

@@ -307,8 +307,9 @@ static uint32_t final_tile_cap(const FfaXform& X, int smax, bool snr_epilogue, u
 }
 
 void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uint32_t num_widths,
-                     uint64_t scratch_budget, ExecPlan& out, uint32_t max_width)
+                     uint64_t scratch_budget, ExecPlan& out, uint32_t max_width, uint32_t banks)
 {
+    if (banks != 1 && banks != 2) throw std::invalid_argument("scratch banks: 1 or 2");
     out = ExecPlan();
     out.xf = xforms;
     for (const FfaXform& X : xforms) {
@@ -318,6 +319,7 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
                                         " floats exceeds the 2 GiB range of the cone kernel");
     }
     const size_t nx = xforms.size();
+    std::vector<uint32_t> xgroup(nx, 0);
     size_t g0 = 0;
     uint32_t group = 0;
     std::vector<std::vector<PassItems>> sched;
@@ -329,6 +331,7 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
             const uint64_t cells = ((uint64_t)xforms[g1].m * xforms[g1].p + 3) & ~(uint64_t)3;
             if (g1 > g0 && scratch + cells > scratch_budget) break;
             out.xf[g1].buf_off = scratch;
+            xgroup[g1] = group;
             scratch += cells;
             ++g1;
         }
@@ -341,6 +344,7 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
             gpasses = std::max<uint32_t>(gpasses, (uint32_t)sched[i - g0].size());
         }
         out.max_passes = std::max(out.max_passes, gpasses);
+        const size_t first_launch = out.launches.size();
         // one launch per (pass, kernel variant): a variant runs rows of exactly
         // its slot width (buckets <= 5), so no lane-slot is wasted
         std::vector<int> buckets;
@@ -425,8 +429,23 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
                 out.launches.push_back(L);
             }
         }
+        // within the group: every merge-only launch first (in pass order),
+        // then the final ones -- a final launch of pass k reads only the
+        // merge-only pass k - 1 output of its own transform, so the order is
+        // valid, and a second group can run its merge-only launches while
+        // this group runs its finals (co-scheduling)
+        std::stable_partition(out.launches.begin() + first_launch, out.launches.end(),
+                              [](const Launch& L) { return L.snr == 0; });
         g0 = g1;
         ++group;
+    }
+    out.groups = group;
+    out.bank_floats = out.scratch_floats;
+    out.banks = group > 1 ? banks : 1;
+    if (out.banks == 2) {
+        for (size_t i = 0; i < nx; ++i)
+            if (xgroup[i] & 1u) out.xf[i].buf_off += out.bank_floats;
+        out.scratch_floats = 2 * out.bank_floats;
     }
     // host-built metadata of the tile items (trial-independent, shared by a
     // launch's whole batch)
@@ -936,8 +955,11 @@ void validate_exec_plan(const ExecPlan& ex, bool snr_epilogue)
     for (const Launch& L : ex.launches)
         for (uint32_t i = L.first; i < L.first + L.count; ++i)
             last_pass[ex.items[i].xform] = std::max(last_pass[ex.items[i].xform], L.pass);
-    for (const FfaXform& X : ex.xf)
+    for (const FfaXform& X : ex.xf) {
         if ((uint64_t)X.m * X.p * 4u >= kMaxBlockBytes) throw std::runtime_error("schedule: transform block over 2 GiB");
+        if (X.buf_off + (((uint64_t)X.m * X.p + 3) & ~(uint64_t)3) > ex.scratch_floats)
+            throw std::runtime_error("schedule: transform scratch outside the ping/pong buffers");
+    }
     for (const Launch& L : ex.launches) {
         if (L.first + L.count > ex.items.size()) throw std::runtime_error("schedule: launch outside the item list");
         for (uint32_t i = L.first; i < L.first + L.count; ++i) {

@@ -65,8 +65,14 @@ struct ExecPlan {
     std::vector<ConeItem> items;     // tile items: ConeItem::pad = word offset of their blob
     std::vector<Launch> launches;
     std::vector<uint32_t> blob;      // host-built metadata of every tile item (build_tile_blob)
-    uint64_t scratch_floats = 0;     // per ping/pong buffer, per trial
+    uint64_t scratch_floats = 0;     // per ping/pong buffer, per trial (all banks)
     uint32_t max_passes = 0;
+    // scratch banks: 2 = odd transform groups use a second copy of the
+    // scratch (offset bank_floats), so two groups can run at once on two
+    // streams (capi.cpp run_cone_launches: co-scheduling)
+    uint32_t banks = 1;
+    uint64_t bank_floats = 0;
+    uint32_t groups = 0;
 };
 
 // Tile-unit metadata built on the host once per plan (the cone kernel reads
@@ -100,8 +106,10 @@ void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, int smax, std:
 // Transforms are grouped so that each group's scratch fits scratch_budget
 // floats per buffer; a group's passes are consecutive launches.  max_width
 // (the widest boxcar, 0 = unknown) caps final tiles for the S/N's wide stride.
+// banks = 2: odd groups' scratch in a second bank (co-scheduling of two groups).
+// Within a group, every merge-only launch precedes every final (fused S/N) one.
 void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uint32_t num_widths,
-                     uint64_t scratch_budget, ExecPlan& out, uint32_t max_width = 0);
+                     uint64_t scratch_budget, ExecPlan& out, uint32_t max_width = 0, uint32_t banks = 1);
 
 // Schedule invariants (every item fits its LDS / register budget and stays
 // inside its node, the final pass of every transform covers rows [0, m) once,

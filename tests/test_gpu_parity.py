@@ -416,6 +416,35 @@ def test_bench_schedule_cfg2(rt, golden_full, monkeypatch):
     _check_full_snrs(rt, g, c, one, periods, foldbins, got[0].cpu().numpy())
 
 
+@pytest.mark.parametrize("budget", ["384", "96"])
+def test_cosched_schedule_cfg2(rt, golden_full, monkeypatch, budget):
+    """Co-scheduled transform groups (RIPTIDE_AMD_COSCHED=1: two scratch
+    banks, group g on stream g mod 2, its merge-only launches overlapping
+    group g - 1's final ones) give S/N bit-identical to the one-stream
+    schedule, on the golden cfg2 input and its reverse (batch 2)."""
+    import torch
+    from riptide_amd import engine
+    g = golden_full["configs"]["cfg2"]
+    c = g["case"]
+    raw = inputs.full_input(c)
+    args = (c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"])
+    monkeypatch.setenv("RIPTIDE_AMD_SCRATCH_MFLOATS", budget)
+    monkeypatch.setenv("RIPTIDE_AMD_COSCHED", "1")
+    co = engine.PeriodogramPlan.for_search(*args, ducy_max=c["ducy_max"])
+    monkeypatch.delenv("RIPTIDE_AMD_COSCHED")
+    monkeypatch.delenv("RIPTIDE_AMD_SCRATCH_MFLOATS")
+    ref = engine.PeriodogramPlan.for_search(*args, ducy_max=c["ducy_max"])
+    d = torch.from_numpy(np.stack([raw, raw[::-1].copy()])).cuda()
+    x = engine.deredden_normalise(d, int(round(4.0 / c["tsamp"])), 101)
+    for _ in range(2):                      # the second run reuses the plan's side stream
+        got = co.run(x, check=True)
+        want = ref.run(x, check=True)
+        torch.cuda.synchronize()
+        assert torch.equal(got, want), "co-scheduled groups differ from the one-stream schedule"
+    periods, foldbins = co.grid()
+    _check_full_snrs(rt, g, c, co, periods, foldbins, got[0].cpu().numpy())
+
+
 # ---------------------------------------------------------------- device peak detection (SURVEY.md §8 f1)
 def _device_vs_host_peaks(rt, plan, snr_dev, tobs, dm=0.0, **kw):
     from riptide_amd.peaks import PeakFinder

@@ -269,6 +269,8 @@ def _asan_cases():
     w2 = len(generate_width_trials(c2["bmin"], ducy_max=c2["ducy_max"], wtsp=1.5))
     cases.append(("cfg2-bench-1536M", ["pgram", c2["n"], c2["tsamp"], c2["pmin"], c2["pmax"], c2["bmin"], c2["bmax"], w2],
                   {"RIPTIDE_AMD_SCRATCH_MFLOATS": "1536"}))
+    cases.append(("cfg2-cosched-384M", ["pgram", c2["n"], c2["tsamp"], c2["pmin"], c2["pmax"], c2["bmin"], c2["bmax"], w2],
+                  {"RIPTIDE_AMD_SCRATCH_MFLOATS": "384", "RIPTIDE_AMD_COSCHED": "1"}))
     c5 = inputs.CFG5
     for r in c5["ranges"]:
         f = r["ffa_search"]
@@ -302,8 +304,8 @@ def test_asan_schedule_check():
 
     def run(case):
         name, argv, extra = case
-        env = dict(env0, **extra)
-        env.pop("RIPTIDE_AMD_SCRATCH_MFLOATS", None) if not extra else None
+        env = {k: v for k, v in env0.items() if k not in ("RIPTIDE_AMD_SCRATCH_MFLOATS", "RIPTIDE_AMD_COSCHED")}
+        env.update(extra)
         r = subprocess.run([exe] + [str(a) for a in argv], env=env, capture_output=True, text=True, timeout=600)
         return name, argv, r
 

@@ -9,7 +9,7 @@
 #   bash tools/gpu_run.sh TAG pmc [CFG]              PMC passes (4 counter groups) -> profiles/TAG_pmc_cone[_CFG].json
 #   bash tools/gpu_run.sh TAG configs [LIB...]       per-config table (tools/bench_configs.py) per library
 #   bash tools/gpu_run.sh TAG ab CFG LIB...          same-box A/B of builds: cone ms per trial, alternated twice
-#                                                    (AB_FLAGS=v1,v2: RIPTIDE_AMD_CONE_FLAGS values per build)
+#                                                    (AB_FLAGS=v1,v2: values of AB_VAR, default RIPTIDE_AMD_CONE_FLAGS)
 #   bash tools/gpu_run.sh TAG flags CFG FLAGS...     same-box A/B of RIPTIDE_AMD_CONE_FLAGS values
 #   bash tools/gpu_run.sh TAG stamps CFG             per-phase stamps (libriptide_amd_stamps.so)
 #   bash tools/gpu_run.sh TAG trace LIB...           per-launch cone durations of the cfg2 bench per library
@@ -90,7 +90,7 @@ do_ab() {      # CFG LIB...
   for rep in 1 2; do
     for lib in "$@"; do
       local r
-      r=$(RIPTIDE_AMD_LIB=$lib timeout -k 10 300 python -u tools/ab_env.py RIPTIDE_AMD_CONE_FLAGS "${AB_FLAGS:-7}" "$cfg" 2>&1 | grep '"round": 1') \
+      r=$(RIPTIDE_AMD_LIB=$lib timeout -k 10 300 python -u tools/ab_env.py "${AB_VAR:-RIPTIDE_AMD_CONE_FLAGS}" "${AB_FLAGS:-7}" "$cfg" 2>&1 | grep '"round": 1') \
         || { echo "$lib failed"; exit 1; }
       echo "$r" | sed "s|^|$(basename "$lib") |" | tee -a "$O/ab_$cfg.log"
     done
