@@ -34,10 +34,7 @@ namespace rt {
 // layouts were measured slower: DESIGN.md section 5.)  The merged levels are
 // dense rows (stride p).
 constexpr int kConeWgsPerCu = 2;
-#ifndef RT_CONE_WAVES
-#define RT_CONE_WAVES 8
-#endif
-constexpr int kConeBlock = 64 * RT_CONE_WAVES;
+constexpr int kConeBlock = 512;
 static_assert(kConeBlock % 64 == 0, "whole waves");
 constexpr int kConeWaves = kConeBlock / 64;
 constexpr int kConeWavesPerSimd = kConeWgsPerCu * kConeWaves / 4;
@@ -77,7 +74,7 @@ RT_HD constexpr int snr_group(int p)
     while (G < 64 && ((((p + G - 1) / G) | 1) > kSnrMaxChunk)) G <<= 1;
     return G;
 }
-constexpr int kStageRegs = 45 * 8 / RT_CONE_WAVES;   // merge: staged values per lane (rows x slots)
+constexpr int kStageRegs = 45 * 8 / kConeWaves;   // merge: staged values per lane (rows x slots)
 constexpr int kMaxSlots = 45;               // merge: 64-bin slots per row (p <= 2880)
 constexpr int kMaxRowsPerWave = 24;         // merge: staged rows per wave
 // header words of a unit's host-built blob (plan.hpp build_tile_blob); a
@@ -149,8 +146,20 @@ RT_HD inline int merge_slots(uint32_t p)
 }
 
 // Row stride of the merge levels above the fill in the short-row variant
-// (kPack2, ffa_kernels.hip merge_step_tasks): odd for p >= 8.
-RT_HD inline int pack_stride(int p) { return p >= 8 ? (p | 1) : p; }
+// (kPack2, ffa_kernels.hip merge_step_tasks).  The interleaved tasks (lane
+// (row, segment s) takes bins s + segs*k, k < 8) write up to 8*segs bins per
+// row, so the stride is >= 8*segs; for 16 <= p <= 32 it is the stride with
+// the fewest LDS bank conflicts of those steps' reads over the cfg4
+// schedule (a host simulation of every task address; 1.05-1.34 x the
+// conflict-free cycles against 1.08-2.25 x at the odd stride p | 1).
+RT_HD inline int pack_stride(int p)
+{
+    if (p < 8) return p;
+    if (p < 16) return p <= 8 ? 9 : 17;
+    if (p <= 32)
+        return p == 16 ? 34 : p < 20 ? 35 : p < 25 ? 36 : p < 28 ? 37 : p == 28 ? 36 : p == 29 ? 37 : 38;
+    return p | 1;
+}
 // 64-lane slots per register row of a merge variant, and rows per slot
 RT_HD constexpr int slot_count(int smax) { return smax == kPack2 ? 1 : smax; }
 RT_HD constexpr int row_pack(int smax) { return smax == kPack2 ? 2 : 1; }
@@ -158,7 +167,7 @@ RT_HD constexpr int row_pack(int smax) { return smax == kPack2 ? 2 : 1; }
 // Register rows per wave the merge stages for a variant (register budget);
 // each register row holds row_pack(smax) output rows.  The 4-slot variant
 // stages 9: its LDS capacity at p >= 240 (9 x 8 waves = 72 >= 16128 / 240).
-constexpr int kRw4 = (72 + RT_CONE_WAVES - 1) / RT_CONE_WAVES;
+constexpr int kRw4 = (72 + kConeWaves - 1) / kConeWaves;
 RT_HD constexpr int merge_rows_per_wave(int smax)
 {
     return smax == 4

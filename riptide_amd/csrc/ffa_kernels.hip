@@ -1268,6 +1268,22 @@ __device__ __forceinline__ void pack_rolled_lut(lds_cptr sp, int o, unsigned lon
     for (int k = 0; k < 4; ++k) x[4 + k] = lds_ld((lds_cptr)(rb + ((e1 >> (8 * k)) & 0xFFu)));
 }
 
+// Interleaved short-row tasks (SEGS = segs >= 2, every step whose output
+// stays in LDS): lane (row, segment s) takes bins s + SEGS * k, k < 8, so the
+// segs lanes of a row read consecutive words of each source row (shared
+// words broadcast) and a 32-lane group of a read touches few distinct rows'
+// words per bank; with the per-p strides of pack_stride the steps' reads run
+// at 1.05-1.34 x the conflict-free LDS cycles instead of 1.08-2.25 x (host
+// simulation of the cfg4 schedule).  Bins past p (8 * SEGS > p) are computed
+// from in-bounds words and written into the row's padding (pack_stride >=
+// 8 * SEGS): never read as data.  The interleaved roll table at
+// kPackLutI: entry x = s + roll (x < p + SEGS) holds the byte offsets
+// 4 ((x + SEGS * e) mod p), e < 8.  The HBM-bound last step of a merge-only
+// pass keeps the contiguous tasks (16-byte stores).
+template <int N> struct IntC { static constexpr int value = N; };
+constexpr int kPackLutI = 128;                // word offset: past the contiguous table's 4p <= 128 words
+static_assert(kPackLutI + 2 * (32 + 4) <= kAuxWords, "short-row roll tables");
+
 __device__ __forceinline__ void build_pack_lut(uint32_t* lut, int p, int tid)
 {
     for (int w = tid; w < 4 * p; w += kConeBlock) {
@@ -1282,14 +1298,38 @@ __device__ __forceinline__ void build_pack_lut(uint32_t* lut, int p, int tid)
         }
         lut[w] = word;
     }
+    const int segs = pack_segments(p);
+    if (segs >= 2)
+        for (int w = tid; w < 2 * (p + segs); w += kConeBlock) {
+            const int x = w >> 1, e0 = 4 * (w & 1);
+            uint32_t word = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                int y = x + segs * (e0 + i);      // < p + 8 segs <= 2p + 7 < 3p
+                y -= y >= p ? p : 0;
+                y -= y >= p ? p : 0;
+                word |= (uint32_t)(4 * y) << (8 * i);
+            }
+            lut[kPackLutI + w] = word;
+        }
 }
 
-template <bool TWO, bool FIRST>
+// task -> (row, segment) of the interleaved layout
+template <int SEGS>
+__device__ __forceinline__ void pack_task_i(int t, int& r, int& seg)
+{
+    r = t / SEGS;
+    seg = t - r * SEGS;
+}
+
+// SEGS = 0: contiguous tasks; SEGS = segs >= 2: interleaved tasks
+template <bool TWO, bool FIRST, int SEGS>
 __device__ __forceinline__ void merge_step_tasks(const UnitCtx& C, const float* src, int p, int qs, int lo, int tid,
                                                  int nrows, float (&v)[kPackTasks][kPackSeg], const int* loff)
 {
-    const lut_cptr plut = (lut_cptr)C.aux0;
-    const int segs = pack_segments(p);
+    const lut_cptr plut = (lut_cptr)(C.aux0 + (SEGS ? kPackLutI : 0));
+    const int segs = SEGS ? SEGS : pack_segments(p);
+    constexpr int ES = SEGS ? SEGS : 1;           // word stride of a task's bins
     const int ntask = nrows * segs;
     const uint32_t* const desc = desc_table(C);
     const int dl = TWO ? 0 : desc_offset(C, lo);
@@ -1302,7 +1342,8 @@ __device__ __forceinline__ void merge_step_tasks(const UnitCtx& C, const float* 
     for (int i = 0; i < kPackTasks; ++i) {
         if (kConeBlock * i + wave0 < ntask) {
             int r, j0;
-            pack_task(min(tid + kConeBlock * i, ntask - 1), segs, p, r, j0);
+            if constexpr (SEGS) pack_task_i<SEGS>(min(tid + kConeBlock * i, ntask - 1), r, j0);   // j0: the segment
+            else pack_task(min(tid + kConeBlock * i, ntask - 1), segs, p, r, j0);
             float x0[kPackSeg], x1[kPackSeg];
             if constexpr (TWO) {
                 // the host-resolved row: source rows q0..q3 of level lo + 2, rolls
@@ -1318,7 +1359,7 @@ __device__ __forceinline__ void merge_step_tasks(const UnitCtx& C, const float* 
                 // table entries first (plain loads), then the volatile reads
                 const unsigned long long e1 = plut[j0 + sH], e2 = plut[j0 + sh], e3 = plut[j0 + sTT];
 #pragma unroll
-                for (int k = 0; k < kPackSeg; ++k) x0[k] = lds_ld(h0 + k);
+                for (int k = 0; k < kPackSeg; ++k) x0[k] = lds_ld(h0 + ES * k);
                 pack_rolled_lut(sp, o1, e1, x1);
                 pack_rolled_lut(sp, o2, e2, x2);
                 pack_rolled_lut(sp, o3, e3, x3);
@@ -1334,7 +1375,7 @@ __device__ __forceinline__ void merge_step_tasks(const UnitCtx& C, const float* 
                 const lds_cptr h0 = sp + ho + j0;
                 const unsigned long long e1 = plut[j0 + (car ? 0 : sh)];
 #pragma unroll
-                for (int k = 0; k < kPackSeg; ++k) x0[k] = lds_ld(h0 + k);
+                for (int k = 0; k < kPackSeg; ++k) x0[k] = lds_ld(h0 + ES * k);
                 pack_rolled_lut(sp, to, e1, x1);
                 // a carried size-1 node adds -0.0 (x + (-0.0) == x: the reference's copy)
 #pragma unroll
@@ -1351,18 +1392,21 @@ __device__ __forceinline__ void merge_step_tasks(const UnitCtx& C, const float* 
 // S/N identical.
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
-template <bool GLOBAL>
+template <bool GLOBAL, int SEGS>
 __device__ __forceinline__ void put_tasks(float* base, int q, const float (&v)[kPackTasks][kPackSeg], int p, int tid,
                                           int nrows, __amdgpu_buffer_rsrc_t rs, uint32_t st_o0)
 {
-    const int segs = pack_segments(p);
+    static_assert(!(GLOBAL && SEGS), "HBM stores take the contiguous tasks");
+    const int segs = SEGS ? SEGS : pack_segments(p);
+    constexpr int ES = SEGS ? SEGS : 1;
     const int ntask = nrows * segs;
     const int wave0 = tid & ~63;
 #pragma unroll
     for (int i = 0; i < kPackTasks; ++i) {
         if (kConeBlock * i + wave0 < ntask) {
             int r, j0;
-            pack_task(min(tid + kConeBlock * i, ntask - 1), segs, p, r, j0);
+            if constexpr (SEGS) pack_task_i<SEGS>(min(tid + kConeBlock * i, ntask - 1), r, j0);
+            else pack_task(min(tid + kConeBlock * i, ntask - 1), segs, p, r, j0);
             if constexpr (GLOBAL) {
                 const uint32_t ob = st_o0 + (uint32_t)(r * p + j0) * 4u;
                 // the task's 8 bins as two 16-byte stores (dword-aligned
@@ -1376,7 +1420,7 @@ __device__ __forceinline__ void put_tasks(float* base, int q, const float (&v)[k
             } else {
                 float* const o = base + r * q + j0;
 #pragma unroll
-                for (int k = 0; k < kPackSeg; ++k) o[k] = v[i][k];
+                for (int k = 0; k < kPackSeg; ++k) o[ES * k] = v[i][k];
             }
         }
     }
@@ -1416,20 +1460,37 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
                 float v[kPackTasks][kPackSeg];
                 const bool first = l == L - 1;
                 const float* src = first ? src0 : base;
-                if (first) {
-                    if (two) merge_step_tasks<true, true>(C, src, p, qs, lo, tid, nrows, v, loff);
-                    else merge_step_tasks<false, true>(C, src, p, qs, lo, tid, nrows, v, loff);
-                } else {
-                    if (two) merge_step_tasks<true, false>(C, src, p, qs, lo, tid, nrows, v, nullptr);
-                    else merge_step_tasks<false, false>(C, src, p, qs, lo, tid, nrows, v, nullptr);
-                }
+                // interleaved tasks unless the step's output goes to HBM
+                const int segs = pack_segments(p);
+                const int inter = (segs >= 2 && !(lo == 0 && st)) ? segs : 0;
+                auto step = [&](auto sc) {
+                    constexpr int S = decltype(sc)::value;
+                    if (first) {
+                        if (two) merge_step_tasks<true, true, S>(C, src, p, qs, lo, tid, nrows, v, loff);
+                        else merge_step_tasks<false, true, S>(C, src, p, qs, lo, tid, nrows, v, loff);
+                    } else {
+                        if (two) merge_step_tasks<true, false, S>(C, src, p, qs, lo, tid, nrows, v, nullptr);
+                        else merge_step_tasks<false, false, S>(C, src, p, qs, lo, tid, nrows, v, nullptr);
+                    }
+                };
+                if (inter == 2) step(IntC<2>{});
+                else if (inter == 3) step(IntC<3>{});
+                else if (inter == 4) step(IntC<4>{});
+                else step(IntC<0>{});
                 l = lo - 1;
                 if (lo == 0 && st) {
-                    put_tasks<true>(base, qs, v, p, tid, nrows, rs, st_o0);
+                    put_tasks<true, 0>(base, qs, v, p, tid, nrows, rs, st_o0);
                     return;
                 }
                 if (!(flags & kConeDiagNoBarrier)) lds_barrier();
-                if (!(flags & kConeDiagNoWrite)) put_tasks<false>(base, qs, v, p, tid, nrows, rs, st_o0);
+                // the output level (lo == 0) at the caller's stride qout
+                if (!(flags & kConeDiagNoWrite)) {
+                    const int qw = lo == 0 ? qout : qs;
+                    if (inter == 2) put_tasks<false, 2>(base, qw, v, p, tid, nrows, rs, st_o0);
+                    else if (inter == 3) put_tasks<false, 3>(base, qw, v, p, tid, nrows, rs, st_o0);
+                    else if (inter == 4) put_tasks<false, 4>(base, qw, v, p, tid, nrows, rs, st_o0);
+                    else put_tasks<false, 0>(base, qw, v, p, tid, nrows, rs, st_o0);
+                }
                 if (!(flags & kConeDiagNoBarrier)) lds_barrier();
             }
             return;
@@ -1673,6 +1734,29 @@ __device__ __forceinline__ float snr_std6(const float (&z)[CH + kSnrWin], const 
 }
 #undef RT_MAX6_STEP
 
+// The short rows' standard ladder 1, 2, 3 (generate_width_trials from 16-32
+// bins: BASELINE configs[3]) in 4-lane groups: three independent window
+// maxima and one interleaved quad all-reduce (each DPP reads a register
+// written three instructions earlier), instead of a width switch and an
+// all-reduce with its wait states per width.  Same float operations.
+#define RT_MAX3_STEP(CTRL)                                                                                  \
+    asm volatile("v_max_f32_dpp %0, %0, %0 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                        \
+                 "v_max_f32_dpp %1, %1, %1 " CTRL " row_mask:0xf bank_mask:0xf\n\t"                        \
+                 "v_max_f32_dpp %2, %2, %2 " CTRL " row_mask:0xf bank_mask:0xf"                              \
+                 : "+v"(m[0]), "+v"(m[1]), "+v"(m[2]))
+
+template <int CH>
+__device__ __forceinline__ float snr_std3(const float (&z)[CH + kSnrWin], const float (&cp)[CH], int g)
+{
+    float m[3] = {window_max_nv<CH, 1>(z, cp), window_max_nv<CH, 2>(z, cp), window_max_nv<CH, 3>(z, cp)};
+    asm volatile("s_nop 1" ::: "memory");
+    RT_MAX3_STEP("quad_perm:[1,0,3,2]");
+    RT_MAX3_STEP("quad_perm:[2,3,0,1]");
+    return g == 0 ? m[0] : (g == 1 ? m[1] : m[2]);
+}
+#undef RT_MAX3_STEP
+
+
 #ifdef RT_STAMPS
 #define RT_SNR_MARK(i)                                                           \
     do {                                                                         \
@@ -1769,6 +1853,10 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
     bool std6 = nw >= 6;
 #pragma unroll
     for (int i = 0; i < 6; ++i) std6 = std6 && __builtin_amdgcn_readlane(wlane, i) == kStdWidths[i];
+    // ... or begin 1, 2, 3 in 4-lane groups (short rows)
+    bool std3 = G == 4 && nw >= 3;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) std3 = std3 && __builtin_amdgcn_readlane(wlane, i) == kStdWidths[i];
     for (int base = 0; base < nev; base += rows_per_pass) {
         // opaque per row pass: the column masks (i < cnt, j0 + k >= p) are
         // recomputed by one v_cmp each instead of being hoisted out of the
@@ -1909,6 +1997,13 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
                     iw0 = 6;
                 }
             }
+            if constexpr (G == 4) {
+                if (std3) {
+                    // widths 0-2 are 1, 2, 3: lane g < 3 keeps width g
+                    sel[0] = snr_std3<CH>(z, cp, g);
+                    iw0 = 3;
+                }
+            }
             for (uint32_t iw = iw0; iw < nw; ++iw) {
                 const int w = __builtin_amdgcn_readlane(wlane, (int)iw);
                 if (w <= kSnrWin) emit(iw, window_dispatch<CH>(w, z, cp));
@@ -1996,6 +2091,27 @@ constexpr bool variant_has_group(int smax, int G)
 // box, cone ms per cfg4 trial (profiles/r03zf_ab_cfg4.log): G = 8 0.837 /
 // 0.837, G = 4 0.777 / 0.778, G = 2 0.796 / 0.797, S/N identical -- 4.
 constexpr int kSnrShortG = 4;
+
+// register chunk of a short row's S/N lane (snr_epilogue's kPack2 case)
+__device__ __forceinline__ int snr_short_ch(int p)
+{
+    const int cs = ((p + kSnrShortG - 1) / kSnrShortG) | 1;
+    return cs <= 5 ? 5 : (cs <= 9 ? 9 : kSnrMaxChunk);
+}
+
+// Row stride of a short-row final pass's output level: room for the S/N's
+// whole-chunk prefix writes and its wrapped prefix extension (snr_rows'
+// wfull / ext / natural paths: no per-column dummy selects, no wrap selects
+// in the window reads), and = 4 (mod 8), so the 8 rows x 4 chunks of a 32-lane
+// LDS group (chunk stride c odd) start on 32 distinct banks (at the odd merge
+// stride p | 1 they collided).
+__device__ __forceinline__ int snr_short_stride(int p)
+{
+    const int cs = ((p + kSnrShortG - 1) / kSnrShortG) | 1;
+    const int ch = snr_short_ch(p);
+    const int q0 = max(p + max(ch, kSnrWin), (kSnrShortG - 1) * cs + ch);
+    return q0 + ((4 - q0) & 7);
+}
 
 template <int SMAX, bool WIDE = false>
 __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& U, float* data, int q, const int* wl,
@@ -2204,8 +2320,17 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
         int qout = p;
         // short rows in (row, segment) tasks: every level above the fill at
         // the odd stride pack_stride(p)
-        if constexpr (SMAX == kPack2)
+        if constexpr (SMAX == kPack2) {
             if (L > 0) qout = pack_stride(p);
+            // a final pass's output level at the short-row S/N stride where
+            // the unit's rows fit (over the blob: the blob is dead once the
+            // last merge step has read its table, a barrier before the
+            // level's write-back)
+            if (SNR && L > 0 && p >= kPackSeg && (a.flags & kConeSnrStride)) {
+                const int qf = snr_short_stride(p);
+                if (n0 * qf <= kLdsDataFloats) qout = qf;
+            }
+        }
         if constexpr (SMAX <= 5 && SMAX != kPack2) {
             // = 16 (mod 32) and >= p + kSnrMaxChunk (room for the S/N's whole-
             // chunk prefix writes and its wrapped prefix extension), else >=

@@ -50,7 +50,11 @@ def test_ffa2_golden_bit_exact(rt, golden, m, p, seed):
 
 @pytest.mark.parametrize("m,p", [(1, 1), (2, 1), (7, 3), (33, 64), (150, 260), (1023, 34), (1025, 34),
                                  (5000, 260), (21474, 240), (134217, 16), (3000, 17), (777, 4000),
-                                 (40, 12000), (9, 70000)])
+                                 (40, 12000), (9, 70000),
+                                 # short rows: every interleaved-task segment count (p = 9-32) with p
+                                 # a multiple of 8 and not (bins past p land in the row padding)
+                                 (999, 9), (1500, 12), (5000, 20), (4099, 24), (2049, 27), (3001, 31),
+                                 (65537, 32)])
 def test_ffa2_vs_oracle(rt, oracle, m, p):
     x = np.random.RandomState(m * 31 + p).normal(size=(m, p)).astype(np.float32)
     assert np.array_equal(rt.ffa2(x), oracle.ffa2(x))
