@@ -378,6 +378,8 @@ def bench_cfg3(args, torch, dist, world, rank, local, dev):
         elapsed = rank_max(torch, dist, elapsed, dev)
     cone = engine.profile_read(0)
     stats = plan.stats()
+    # the last batch's first trial through the default-schedule plan
+    checked = None if args.no_self_check else self_check(torch, dist, engine, plan, xbuf, snr, c, local, world, dev)
     if rank == 0:
         pmc, pmc_reason = pmc_traffic("cfg3")
         rf = roofline(engine, cone, stats, B, pmc, pmc_reason)
@@ -405,6 +407,7 @@ def bench_cfg3(args, torch, dist, world, rank, local, dev):
                 "parallelism": f"dm-trials x{world} (round-robin shard of one job, strong scaling)" + REHEARSAL,
             },
             "roofline": rf,
+            "checked": checked,
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baselines("cfg3")
@@ -439,11 +442,11 @@ def main():
 
     # transform-group scratch per ping/pong buffer and trial (capi.cpp
     # scratch_budget_floats, tools/ab_sched.py): cfg2 at 1536 M floats puts
-    # the whole plan in one group, 14 cone launches per step instead of 51 at
+    # the whole plan in one group, 16 cone launches per step instead of 53 at
     # 384 M, 2.5 % faster (profiles/r03zd_sched_cfg2.jsonl), for 175 GB of
     # workspace at 16 trials (53 GB at 384 M), so only where it fits: one
     # workspace, one rank per GPU, and enough free HBM (checked below); cfg3
-    # at 32 trials has 14 launches at 384 M already
+    # at 32 trials has few launches at 384 M already
     user_scratch = "RIPTIDE_AMD_SCRATCH_MFLOATS" in os.environ
     if args.workload in ("cfg2", "cfg3"):
         big = args.workload == "cfg2" and not args.overlap and not args.one_gpu_rehearsal

@@ -16,7 +16,7 @@
 #   bash tools/gpu_run.sh TAG parity LIB...          GPU parity tests (test_gpu_parity.py) per library
 #   bash tools/gpu_run.sh TAG pmcflags CFG FLAGS...  instruction counters per RIPTIDE_AMD_CONE_FLAGS value
 #                                                    (diagnostic bits: phase attribution of VALU / SALU / LDS)
-#   bash tools/gpu_run.sh TAG round                  round-end pass: pmc (cfg2, cfg3), tests, smoke,
+#   bash tools/gpu_run.sh TAG round                  round-end pass: pmc (cfg2, cfg3, cfg4), tests, smoke,
 #                                                    bench cfg2 / cfg3 / cfg5, configs, prof
 set -o pipefail
 TAG=$1; CMD=$2; shift 2
@@ -180,6 +180,7 @@ case "$CMD" in
   round)
     do_pmc cfg2
     do_pmc cfg3
+    do_pmc cfg4
     do_tests
     do_bench bench
     do_bench bench_cfg3 --workload cfg3
