@@ -278,7 +278,8 @@ def _asan_cases():
         cases.append((f"cfg5-{r['name']}", ["pgram", c5["n"], c5["tsamp"], f["period_min"], f["period_max"],
                                             f["bins_min"], f["bins_max"], w], {}))
     for m, p in [(1, 1), (2, 1), (7, 3), (33, 64), (150, 260), (1023, 34), (1025, 34), (5000, 260), (21474, 240),
-                 (134217, 16), (3000, 17), (777, 4000), (40, 12000), (9, 70000)]:
+                 (134217, 16), (3000, 17), (777, 4000), (40, 12000), (9, 70000),
+                 (999, 9), (1500, 12), (5000, 20), (4099, 24), (2049, 27), (3001, 31), (65537, 32)]:
         cases.append((f"ffa-{m}x{p}", ["ffa", m, p], {}))
     for m, p, _ in inputs.FFA_CASES:
         cases.append((f"ffa-{m}x{p}", ["ffa", m, p], {}))
