@@ -178,13 +178,6 @@ RT_HD constexpr int merge_rows_per_wave(int smax)
                                                                          : kMaxRowsPerWave));
 }
 
-// Whole-node launches of the 4- and 5-slot variants are split by node size
-// into launches of kernel instances staging ceil(rows / 8) register rows per
-// wave (kMinRw .. the default): the merge computes every register row on
-// every level, so a 9-row instance on 33-48-row nodes would compute 3-4
-// dropped rows per wave and level.
-constexpr int kMinRw = 5;
-
 // Row capacity of one cone work unit for p phase bins run by the kernel
 // variant smax (merge_slots(p), or a wider slot width): the level buffer, and
 // the register staging of a level (merge_rows_per_wave(smax) register rows

@@ -2426,35 +2426,15 @@ hipError_t launch_cone(const ConeArgs& args, uint32_t smax, uint32_t rw, bool wi
     if (total > 0xFFFFFFFFull) return hipErrorInvalidValue;
     const dim3 g((uint32_t)total), b(kConeBlock);
     hipError_t e = hipErrorInvalidValue;
+    // one instance per slot width: every unit runs the variant's default
+    // register rows (the planner no longer splits launches by node size)
+    if (rw != 0) return hipErrorInvalidValue;
     switch (smax) {
-    case 1:
-        switch (rw) {
-        case 12: e = launch_kind<1, 12>(args, g, b, wide_snr, snr, s); break;
-        case 16: e = launch_kind<1, 16>(args, g, b, wide_snr, snr, s); break;
-        case 20: e = launch_kind<1, 20>(args, g, b, wide_snr, snr, s); break;
-        default: e = launch_kind<1>(args, g, b, wide_snr, snr, s); break;
-        }
-        break;
+    case 1: e = launch_kind<1>(args, g, b, wide_snr, snr, s); break;
     case 2: e = launch_kind<2>(args, g, b, wide_snr, snr, s); break;
     case 3: e = launch_kind<3>(args, g, b, wide_snr, snr, s); break;
-    case 4:
-        switch (rw) {
-        case 5: e = launch_kind<4, 5>(args, g, b, wide_snr, snr, s); break;
-        case 6: e = launch_kind<4, 6>(args, g, b, wide_snr, snr, s); break;
-        case 7: e = launch_kind<4, 7>(args, g, b, wide_snr, snr, s); break;
-        case 8: e = launch_kind<4, 8>(args, g, b, wide_snr, snr, s); break;
-        default: e = launch_kind<4>(args, g, b, wide_snr, snr, s); break;
-        }
-        break;
-    case 5:
-        switch (rw) {
-        case 5: e = launch_kind<5, 5>(args, g, b, wide_snr, snr, s); break;
-        case 6: e = launch_kind<5, 6>(args, g, b, wide_snr, snr, s); break;
-        case 7: e = launch_kind<5, 7>(args, g, b, wide_snr, snr, s); break;
-        case 8: e = launch_kind<5, 8>(args, g, b, wide_snr, snr, s); break;
-        default: e = launch_kind<5>(args, g, b, wide_snr, snr, s); break;
-        }
-        break;
+    case 4: e = launch_kind<4>(args, g, b, wide_snr, snr, s); break;
+    case 5: e = launch_kind<5>(args, g, b, wide_snr, snr, s); break;
     case 8: e = launch_kind<8>(args, g, b, wide_snr, snr, s); break;
     case 16: e = launch_kind<16>(args, g, b, wide_snr, snr, s); break;
     case kMaxSlots: e = launch_kind<kMaxSlots>(args, g, b, wide_snr, snr, s); break;

@@ -389,43 +389,10 @@ void build_exec_plan(const std::vector<FfaXform>& xforms, bool snr_epilogue, uin
                                      return item_cost(x, out.xf[x.xform]) > item_cost(y, out.xf[y.xform]);
                                  });
                 if (!L.count) continue;
-                if (k == 0 && (bucket == 1 || bucket == 4 || bucket == 5) && merge_rows_per_wave(bucket) > kMinRw) {
-                    // whole-node pass: one launch per register-row class
-                    // ceil(node rows / 8) (bytes split by cells); the 1-slot
-                    // variant (24 rows) in classes of 4 rows from 12
-                    const int rwd = merge_rows_per_wave(bucket);
-                    auto rw_of = [&](const ConeItem& x) {
-                        int r = ((int)x.node_size + kConeWaves - 1) / kConeWaves;
-                        if (bucket == 1) r = r <= 12 ? 12 : (r + 3) / 4 * 4;
-                        return r < kMinRw ? kMinRw : r;
-                    };
-                    auto b0 = out.items.begin() + L.first, b1 = out.items.end();
-                    std::stable_sort(b0, b1, [&](const ConeItem& x, const ConeItem& y) { return rw_of(x) > rw_of(y); });
-                    double ct = 0;
-                    for (auto it = b0; it != b1; ++it) ct += (double)it->node_size * out.xf[it->xform].p;
-                    uint32_t f0 = L.first;
-                    uint64_t cells_left = L.cells;
-                    while (f0 < L.first + L.count) {
-                        const int r = rw_of(out.items[f0]);
-                        uint32_t f1 = f0;
-                        double c = 0;
-                        while (f1 < L.first + L.count && rw_of(out.items[f1]) == r) {
-                            c += (double)out.items[f1].node_size * out.xf[out.items[f1].xform].p;
-                            ++f1;
-                        }
-                        Launch S = L;
-                        S.first = f0;
-                        S.count = f1 - f0;
-                        S.rw = r >= rwd ? 0u : (uint32_t)r;
-                        S.alg_bytes = L.alg_bytes * c / ct;
-                        S.moved_bytes = L.moved_bytes * c / ct;
-                        S.cells = f1 < L.first + L.count ? (uint64_t)((double)L.cells * c / ct) : cells_left;
-                        cells_left -= S.cells;
-                        out.launches.push_back(S);
-                        f0 = f1;
-                    }
-                    continue;
-                }
+                // whole-node units of every size in one launch, longest first
+                // (one launch per register-row class, as before round 4, left
+                // CUs idle at each class's drain: cfg2 7.22 -> 7.10, cfg3
+                // 1.864 -> 1.809, cfg1 0.285 -> 0.263 ms per trial, same S/N)
                 out.launches.push_back(L);
             }
         }
