@@ -442,7 +442,7 @@ def main():
 
     # transform-group scratch per ping/pong buffer and trial (capi.cpp
     # scratch_budget_floats, tools/ab_sched.py): cfg2 at 1536 M floats puts
-    # the whole plan in one group, 16 cone launches per step instead of 53 at
+    # the whole plan in one group, 8 cone launches per step instead of 26 at
     # 384 M, 2.5 % faster (profiles/r03zd_sched_cfg2.jsonl), for 175 GB of
     # workspace at 16 trials (53 GB at 384 M), so only where it fits: one
     # workspace, one rank per GPU, and enough free HBM (checked below); cfg3
