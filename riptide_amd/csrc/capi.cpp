@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <map>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -334,7 +335,57 @@ void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStrea
     a.blob = P.d_blob;
     const std::vector<Launch>& Ls = P.ex.launches;
     if (P.ex.banks < 2 || P.ex.groups < 2) {
-        for (const Launch& L : Ls) cone_launch(P, L, a, batch, s, true);
+        bool multi = false;
+        for (const Launch& L : Ls) multi = multi || L.smax != Ls.front().smax;
+        if (!multi) {
+            for (const Launch& L : Ls) cone_launch(P, L, a, batch, s, true);
+            return;
+        }
+        // slot-width buckets on two streams: within a transform group the
+        // launches of different slot widths belong to disjoint transforms
+        // (independent pass chains), so the group's main bucket (most cells)
+        // runs on s and the others on a side stream, joined at the group's
+        // end (the next group reuses the scratch buffers).  Each chain's
+        // launch drains fill with the other's units: cone ms per trial cfg2
+        // 7.092 -> 7.072, cfg3 1.795 -> 1.776, cfg1 0.274 -> 0.260
+        // (profiles/r04r_ab_*_bucketstreams.log); the cone time is then one
+        // profiling record from the fork to the join.
+        const uint32_t G = std::max<uint32_t>(P.ex.groups, 1);
+        SideSet* ss = P.take_side(2 * (size_t)G);
+        ProfRec r{};
+        const bool prof = g_prof.on;
+        if (prof) {
+            {
+                std::lock_guard<std::mutex> lk(g_prof.mu);
+                r.a = g_prof.ev();
+                r.b = g_prof.ev();
+            }
+            for (const Launch& L : Ls) {
+                r.alg += L.alg_bytes * batch;
+                r.moved += L.moved_bytes * batch;
+            }
+            ck(hipEventRecord(r.a, s), "hipEventRecord");
+        }
+        size_t li = 0;
+        for (uint32_t g = 0; g < G && li < Ls.size(); ++g) {
+            size_t l1 = li;
+            std::map<uint32_t, uint64_t> cells;
+            while (l1 < Ls.size() && Ls[l1].group == Ls[li].group) cells[Ls[l1].smax] += Ls[l1].cells, ++l1;
+            uint32_t mainb = Ls[li].smax;
+            for (const auto& kv : cells) if (kv.second > cells[mainb]) mainb = kv.first;
+            ck(hipEventRecord(ss->ev[2 * g], s), "hipEventRecord");
+            ck(hipStreamWaitEvent(ss->s2, ss->ev[2 * g], 0), "hipStreamWaitEvent");
+            for (; li < l1; ++li) cone_launch(P, Ls[li], a, batch, Ls[li].smax == mainb ? s : ss->s2, false);
+            ck(hipEventRecord(ss->ev[2 * g + 1], ss->s2), "hipEventRecord");
+            ck(hipStreamWaitEvent(s, ss->ev[2 * g + 1], 0), "hipStreamWaitEvent");
+        }
+        if (li != Ls.size()) throw std::runtime_error("cone launches out of group order");
+        P.give_side(ss);
+        if (prof) {
+            ck(hipEventRecord(r.b, s), "hipEventRecord");
+            std::lock_guard<std::mutex> lk(g_prof.mu);
+            g_prof.rec[0].push_back(r);
+        }
         return;
     }
     const uint32_t G = P.ex.groups;
