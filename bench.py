@@ -545,7 +545,13 @@ def main():
         trials = world * B * args.steps
         rf = roofline(engine, cone, stats, B, pmc, pmc_reason)
         rf["kernel_ms_per_step"] = cone["ms"] / args.steps
-        rf["kernel_launches_per_step"] = cone["launches"] / args.steps
+        # one HIP-event record per cone launch, or one per launch sequence
+        # when the plan's slot-width chains run on two streams (capi.cpp
+        # run_cone_launches): then `achieved` is the sequence's algorithmic
+        # bytes over its wall time, the two chains overlapping
+        rf["profile_records_per_step"] = cone["launches"] / args.steps
+        rf["timing"] = ("HIP events per cone launch" if cone["launches"] == stats["launches"] * args.steps
+                        else "HIP events around each step's cone launch sequence (two streams)")
         rf["ladder_ms_per_step"] = ladder["ms"] / args.steps
         line = {
             "metric": METRIC,
