@@ -384,6 +384,9 @@ def bench_cfg3(args, torch, dist, world, rank, local, dev):
         pmc, pmc_reason = pmc_traffic("cfg3")
         rf = roofline(engine, cone, stats, B, pmc, pmc_reason)
         rf["kernel_ms_per_trial"] = cone["ms"] / (args.steps * len(mine))
+        nb = (len(mine) + B - 1) // B
+        rf["timing"] = ("HIP events per cone launch" if cone["launches"] == stats["launches"] * args.steps * nb
+                        else "HIP events around each batch's cone launch sequence (two streams)")
         line = {
             "metric": "DM trials/sec (node), 1024-trial job at 2^22 samples, P=0.2-5 s (BASELINE configs[2])",
             "value": ntr * args.steps / elapsed,
