@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Aggregate rocprofv3 --pmc per-dispatch CSVs (tools/gpu_pmc.sh) per kernel.
+"""Aggregate rocprofv3 --pmc per-dispatch CSVs (tools/gpu_run.sh TAG pmc) per kernel.
 
 usage: tools/pmc_summary.py gpurun_out/<tag> [kernel-substring]
 Prints, per counter, the sum over the matching kernel's dispatches and the

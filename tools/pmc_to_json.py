@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Turn a tools/gpu_pmc.sh run into profiles/<name>.json: per-trial HBM bytes of
+"""Turn a tools/gpu_run.sh pmc run into profiles/<name>.json: per-trial HBM bytes of
 the cone kernel from FETCH_SIZE / WRITE_SIZE (rocprofv3, KB units), with the
 gfx950 correction of MI355X_MICROARCH.md (FETCH_SIZE reports half the bytes of
 wide streaming reads: x2), plus the SQ counters as ratios.
