@@ -8,8 +8,8 @@
 
 namespace rt {
 
-constexpr uint32_t kDsSpanFloats = 8192;   // LDS input stage of the ladder kernel (32 KiB)
-constexpr uint32_t kDsFusedMargin = 1024;  // fused ladder: staged floats past the span (rungs with ceil(f) + 2 <= margin)
+constexpr uint32_t kDsSpanFloats = 4096;   // LDS input stage of the ladder kernels (16 KiB)
+constexpr uint32_t kDsFusedMargin = 512;   // fused ladder: staged floats past the span (rungs with ceil(f) + 2 <= margin)
 constexpr uint32_t kDsMaxRungs = 256;      // fused ladder: rungs per plan (per-block rung ranges in LDS)
 
 struct DsRung {
