@@ -15,6 +15,7 @@ Prints one JSON line (rank 0).  Launch for N>1:
 """
 import argparse
 import json
+import math
 import os
 import subprocess
 import sys
@@ -140,6 +141,26 @@ def roofline(engine, cone, stats, trials_per_launch_unit, pmc=None, pmc_reason=N
         "alg_bytes_per_trial": stats["alg_bytes"],
         "moved_bytes_per_trial": stats["moved_bytes"],
     }
+
+
+def floor_bytes_per_trial(c, plan, stats):
+    """SURVEY.md §8(d)'s implementation-independent floor of one trial's
+    periodogram: every used rung reads the series and writes its downsampled
+    series once (Σ_rungs 4N + 4n), every transform reads its input block once
+    (4·Σ m·p = 4·cells), the S/N is written once (4·L·W) and the grid once
+    (12·L: periods f64 + foldbins u32).  The rungs follow periodogram.hpp:
+    135-175 (f = f0·g^k, n = floor(N / f), bstop = min(bmax, n, floor(pmax /
+    tau)); a rung with bstop < bmin feeds no transform)."""
+    n_in, tsamp = c["n"], c["tsamp"]
+    f0 = c["pmin"] / (tsamp * c["bmin"])
+    g = (c["bmax"] + 1.0) / c["bmin"]
+    rung_bytes = 0
+    for k in range(int(math.ceil(math.log(c["pmax"] / c["pmin"]) / math.log(g)))):
+        f = f0 * g ** k
+        n = int(math.floor(n_in / f))
+        if min(c["bmax"], n, int(c["pmax"] / (f * tsamp))) >= c["bmin"]:
+            rung_bytes += 4 * n_in + 4 * n
+    return rung_bytes + 4 * stats["cells"] + 4 * plan.length * plan.num_widths + 12 * plan.length
 
 
 def _drop_cache(fn):
@@ -387,6 +408,11 @@ def bench_cfg3(args, torch, dist, world, rank, local, dev):
         nb = (len(mine) + B - 1) // B
         rf["timing"] = ("HIP events per cone launch" if cone["launches"] == stats["launches"] * args.steps * nb
                         else "HIP events around each batch's cone launch sequence (two streams)")
+        fb = floor_bytes_per_trial(c, plan, stats)
+        rf["floor_bytes_per_trial"] = fb
+        rf["floor_frac"] = fb * ntr * args.steps / elapsed / 1e9 / HBM_PEAK_GBS
+        rf["floor_basis"] = ("SURVEY.md §8(d): Σ_rungs(4N + 4n) + 4·Σ m·p + 4·L·W + 12·L per trial, x trials "
+                             "/ wall time of the job / peak")
         line = {
             "metric": "DM trials/sec (node), 1024-trial job at 2^22 samples, P=0.2-5 s (BASELINE configs[2])",
             "value": ntr * args.steps / elapsed,
@@ -556,6 +582,13 @@ def main():
         rf["timing"] = ("HIP events per cone launch" if cone["launches"] == stats["launches"] * args.steps
                         else "HIP events around each step's cone launch sequence (two streams)")
         rf["ladder_ms_per_step"] = ladder["ms"] / args.steps
+        # progress against the implementation-independent floor (VERDICT r4:
+        # the per-pass `frac` above rises if the schedule adds passes)
+        fb = floor_bytes_per_trial(c, plan, stats)
+        rf["floor_bytes_per_trial"] = fb
+        rf["floor_frac"] = fb * trials / elapsed / 1e9 / HBM_PEAK_GBS
+        rf["floor_basis"] = ("SURVEY.md §8(d): Σ_rungs(4N + 4n) + 4·Σ m·p + 4·L·W + 12·L per trial, x trials "
+                             "/ wall time of the timed steps / peak")
         line = {
             "metric": METRIC,
             "value": trials / elapsed,

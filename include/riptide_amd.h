@@ -101,7 +101,7 @@ int rt_fast_running_median(const float* x, size_t size, size_t width_samples, si
 int rt_deredden_normalise(const float* x, size_t size, size_t width_samples, size_t min_points,
                           int deredden, int normalise, float* out);
 
-/* periodogram.hpp:260-264  trial-period grid only (host computation, no device) */
+/* periodogram.hpp:190-194  trial-period grid only (host computation, no device) */
 int rt_periodogram_grid(size_t size, double tsamp, double period_min, double period_max, size_t bins_min,
                         size_t bins_max, double* periods, uint32_t* foldbins);
 

@@ -16,6 +16,7 @@
  * Citations are path:line relative to /root/reference.
  */
 #include <math.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -199,7 +200,7 @@ int oracle_snr2(const float* x, size_t rows, size_t cols, const uint64_t* widths
 }
 
 /* ------------------------------------------------------------------------- */
-/* Periodogram plan and grid (periodogram.hpp:54-271)                         */
+/* Periodogram plan and grid (periodogram.hpp:54-201)                         */
 /* ------------------------------------------------------------------------- */
 static size_t ceilshift(size_t rows, size_t cols, double pmax)
 {
@@ -272,7 +273,7 @@ size_t oracle_periodogram_length(size_t n, double tsamp, double pmin, double pma
 
 /* Grid form selector: 1 = form emitted by the reference build
  *   periods[s] = (B*B*tau) / fma(s, -1/(rows-1), B)
- * 0 = source text of periodogram.hpp:262: tau * B * B / (B - s / (rows - 1.0)) */
+ * 0 = source text of periodogram.hpp:192: tau * B * B / (B - s / (rows - 1.0)) */
 static int g_grid_emitted = 1;
 void oracle_set_grid_emitted(int on) { g_grid_emitted = on; }
 
@@ -309,7 +310,7 @@ static void pgram_cb(const oracle_step* st, void* vctx)
     if (!c->grid_only && st->rows_eval > 0) {
         const float* input = c->data;
         if (!(st->f == 1.0)) {
-            /* the ladder re-reads the original series at every rung (periodogram.hpp:232-238) */
+            /* the ladder re-reads the original series at every rung (periodogram.hpp:162-168) */
             oracle_downsample(c->data, c->size, st->f, c->ds);
             input = c->ds;
         }
@@ -322,7 +323,7 @@ static void pgram_cb(const oracle_step* st, void* vctx)
     c->snrs += st->rows_eval * c->nw;
 }
 
-/* Full periodogram (periodogram.hpp:187-271).  Caller validated arguments and
+/* Full periodogram (periodogram.hpp:117-201).  Caller validated arguments and
  * widths (0 < w < bins_min).  grid_only != 0 skips downsample/FFA/S/N.
  * Returns -1 on allocation failure. */
 int oracle_periodogram(const float* data, size_t size, double tsamp, const uint64_t* widths,
@@ -357,6 +358,164 @@ int oracle_periodogram(const float* data, size_t size, double tsamp, const uint6
     plan_walk(size, tsamp, pmin, pmax, bmin, bmax, pgram_cb, &c);
     free(c.ds); free(c.ffa); free(c.tmp); free(c.cps);
     return 0;
+}
+
+/* The same periodogram on `nthreads` host threads (full-size parity tests:
+ * every one of the L x W values of cfg2 against this checker).  Each rung's
+ * series is downsampled once; the (rung, bins) steps then run on the threads,
+ * each writing its own rows_eval rows of periods / foldbins / snrs.  Per
+ * step the arithmetic is pgram_cb's, so the output is identical to
+ * oracle_periodogram's for any thread count. */
+typedef struct {
+    oracle_step* st;
+    size_t n, cap;
+} step_list;
+
+static void collect_cb(const oracle_step* st, void* ctx)
+{
+    step_list* l = (step_list*)ctx;
+    if (l->n == l->cap) {
+        l->cap = l->cap ? 2 * l->cap : 256;
+        l->st = (oracle_step*)realloc(l->st, l->cap * sizeof(oracle_step));
+    }
+    if (l->st) l->st[l->n++] = *st;
+}
+
+typedef struct {
+    const float* data;
+    size_t size;
+    const uint64_t* widths;
+    size_t nw, bmax, wmax;
+    const step_list* steps;
+    const size_t* row0;          /* first output row of each step */
+    float* const* rung_series;   /* downsampled series of each rung (NULL: f == 1) */
+    size_t nrungs;
+    double* periods;
+    uint32_t* foldbins;
+    float* snrs;
+    size_t next;                 /* next unit of work (rungs, then steps) */
+    pthread_mutex_t mu;
+    int phase;                   /* 0: downsample rungs, 1: steps */
+    int failed;
+} mt_ctx;
+
+static int mt_take(mt_ctx* c, size_t limit, size_t* idx)
+{
+    pthread_mutex_lock(&c->mu);
+    const int ok = c->next < limit;
+    if (ok) *idx = c->next++;
+    pthread_mutex_unlock(&c->mu);
+    return ok;
+}
+
+static void* mt_ladder(void* v)
+{
+    mt_ctx* c = (mt_ctx*)v;
+    size_t r;
+    while (mt_take(c, c->nrungs, &r)) {
+        /* the first step of rung r carries its factor */
+        for (size_t i = 0; i < c->steps->n; ++i)
+            if (c->steps->st[i].rung == r) {
+                const oracle_step* st = &c->steps->st[i];
+                if (c->rung_series[r]) oracle_downsample(c->data, c->size, st->f, c->rung_series[r]);
+                break;
+            }
+    }
+    return NULL;
+}
+
+static void* mt_steps(void* v)
+{
+    mt_ctx* c = (mt_ctx*)v;
+    float* tmp = NULL; float* ffa = NULL; float* cps = NULL;
+    size_t i, bufsize = 0;
+    for (size_t k = 0; k < c->steps->n; ++k) {
+        const size_t cells = c->steps->st[k].rows * c->steps->st[k].bins;
+        if (cells > bufsize) bufsize = cells;
+    }
+    tmp = (float*)malloc((bufsize + 1) * sizeof(float));
+    ffa = (float*)malloc((bufsize + 1) * sizeof(float));
+    cps = (float*)malloc((c->bmax + c->wmax + 1) * sizeof(float));
+    if (!tmp || !ffa || !cps) {
+        c->failed = 1;
+        free(tmp); free(ffa); free(cps);
+        return NULL;
+    }
+    while (mt_take(c, c->steps->n, &i)) {
+        const oracle_step* st = &c->steps->st[i];
+        const size_t B = st->bins, r0 = c->row0[i];
+        for (size_t s = 0; s < st->rows_eval; ++s) {
+            double per;
+            if (g_grid_emitted) {
+                const double num = (double)(B * B) * st->tau;
+                per = num / fma((double)s, -1.0 / ((double)st->rows - 1.0), (double)B);
+            } else {
+                per = st->tau * (double)B * (double)B / ((double)B - (double)s / ((double)st->rows - 1.0));
+            }
+            c->periods[r0 + s] = per;
+            c->foldbins[r0 + s] = (uint32_t)B;
+        }
+        if (st->rows_eval == 0) continue;
+        const float* input = c->rung_series[st->rung] ? c->rung_series[st->rung] : c->data;
+        ffa_rec(input, tmp, ffa, st->rows, B);
+        for (size_t s = 0; s < st->rows_eval; ++s)
+            snr_row(ffa + s * B, B, c->widths, c->nw, st->stdnoise, cps, c->snrs + (r0 + s) * c->nw);
+    }
+    free(tmp); free(ffa); free(cps);
+    return NULL;
+}
+
+int oracle_periodogram_mt(const float* data, size_t size, double tsamp, const uint64_t* widths,
+                          size_t nw, double pmin, double pmax, size_t bmin, size_t bmax,
+                          double* periods, uint32_t* foldbins, float* snrs, int nthreads)
+{
+    step_list steps = {NULL, 0, 0};
+    plan_walk(size, tsamp, pmin, pmax, bmin, bmax, collect_cb, &steps);
+    if (steps.n == 0) return 0;
+    if (!steps.st) return -1;
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    mt_ctx c;
+    memset(&c, 0, sizeof c);
+    c.data = data; c.size = size; c.widths = widths; c.nw = nw; c.bmax = bmax;
+    for (size_t i = 0; i < nw; ++i)
+        if (widths[i] > c.wmax) c.wmax = widths[i];
+    c.steps = &steps;
+    c.periods = periods; c.foldbins = foldbins; c.snrs = snrs;
+    c.nrungs = steps.st[steps.n - 1].rung + 1;
+    size_t* row0 = (size_t*)malloc(steps.n * sizeof(size_t));
+    float** rs = (float**)calloc(c.nrungs, sizeof(float*));
+    int rc = 0;
+    if (!row0 || !rs) rc = -1;
+    for (size_t i = 0, acc = 0; rc == 0 && i < steps.n; ++i) {
+        row0[i] = acc;
+        acc += steps.st[i].rows_eval;
+        const oracle_step* st = &steps.st[i];
+        if (!(st->f == 1.0) && !rs[st->rung]) {
+            rs[st->rung] = (float*)malloc((st->n + 1) * sizeof(float));
+            if (!rs[st->rung]) rc = -1;
+        }
+    }
+    if (rc == 0) {
+        c.row0 = row0;
+        c.rung_series = rs;
+        pthread_mutex_init(&c.mu, NULL);
+        pthread_t th[256];
+        for (int phase = 0; phase < 2 && rc == 0; ++phase) {
+            c.next = 0;
+            int started = 0;
+            for (int t = 0; t < nthreads; ++t, ++started)
+                if (pthread_create(&th[t], NULL, phase ? mt_steps : mt_ladder, &c) != 0) break;
+            if (started == 0) rc = -1;
+            for (int t = 0; t < started; ++t) pthread_join(th[t], NULL);
+            if (c.failed) rc = -1;
+        }
+        pthread_mutex_destroy(&c.mu);
+    }
+    if (rs)
+        for (size_t r = 0; r < c.nrungs; ++r) free(rs[r]);
+    free(rs); free(row0); free(steps.st);
+    return rc;
 }
 
 /* ------------------------------------------------------------------------- */

@@ -175,7 +175,30 @@ std::atomic<int> g_test_corrupt{0};
 // taken by one call at a time from the plan's pool.
 struct SideSet {
     hipStream_t s2 = nullptr;
+    hipEvent_t err_join = nullptr;   // error path: joins s2 back into the caller's stream
     std::vector<hipEvent_t> ev;
+};
+
+// Makes `device` current for a scope and restores the caller's device on
+// exit: the side streams and events of a plan belong to the plan's device,
+// whatever device the calling thread has current.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int device)
+    {
+        int cur = 0;
+        ck(hipGetDevice(&cur), "hipGetDevice");
+        if (cur != device) {
+            ck(hipSetDevice(device), "hipSetDevice");
+            prev = cur;
+        }
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
 };
 
 struct DevicePlan {
@@ -192,12 +215,16 @@ struct DevicePlan {
         if (d_blob) (void)hipFree(d_blob);
         for (auto& ss : side_all) {
             for (hipEvent_t e : ss->ev) (void)hipEventDestroy(e);
+            if (ss->err_join) (void)hipEventDestroy(ss->err_join);
             if (ss->s2) (void)hipStreamDestroy(ss->s2);
         }
     }
+    // A side stream and `events` events on the plan's device (created there
+    // whatever the calling thread's current device is).
     SideSet* take_side(size_t events) const
     {
         std::lock_guard<std::mutex> lk(side_mu);
+        DeviceGuard dg(device);
         SideSet* ss;
         if (!side_free.empty()) {
             ss = side_free.back();
@@ -206,6 +233,7 @@ struct DevicePlan {
             side_all.push_back(std::make_unique<SideSet>());
             ss = side_all.back().get();
             ck(hipStreamCreateWithFlags(&ss->s2, hipStreamNonBlocking), "hipStreamCreate");
+            ck(hipEventCreateWithFlags(&ss->err_join, hipEventDisableTiming), "hipEventCreate");
         }
         while (ss->ev.size() < events) {
             hipEvent_t e;
@@ -320,6 +348,39 @@ void cone_launch(const DevicePlan& P, const Launch& L, ConeArgs a, uint32_t batc
     }
 }
 
+// A side set taken from a plan's pool for one launch sequence: returned to
+// the pool on every exit.  While `forked`, launches may be queued on the side
+// stream that the caller's stream has not joined; an exception then joins
+// them back (so the caller cannot reuse or free the workspace while the side
+// stream still writes it) before the set goes back to the pool.
+struct SideLease {
+    const DevicePlan& P;
+    SideSet* ss;
+    hipStream_t s;
+    bool forked = false;
+    SideLease(const DevicePlan& plan, size_t events, hipStream_t caller) : P(plan), ss(plan.take_side(events)), s(caller) {}
+    ~SideLease()
+    {
+        if (forked) {
+            DeviceGuard dg(P.device);
+            if (hipEventRecord(ss->err_join, ss->s2) != hipSuccess || hipStreamWaitEvent(s, ss->err_join, 0) != hipSuccess)
+                (void)hipStreamSynchronize(ss->s2);
+        }
+        P.give_side(ss);
+    }
+    SideLease(const SideLease&) = delete;
+    SideLease& operator=(const SideLease&) = delete;
+};
+
+// RIPTIDE_AMD_SINGLE_STREAM=1: every cone launch of a plan on the caller's
+// stream, in plan order, one profiling record per launch (per-launch A/B
+// measurements and the parity test of the two-stream scheduling).
+bool single_stream_forced()
+{
+    const char* e = std::getenv("RIPTIDE_AMD_SINGLE_STREAM");
+    return e && e[0] == '1';
+}
+
 // Run all cone launches of an exec plan.  A plan with two scratch banks
 // (ExecPlan::banks) runs its transform groups co-scheduled on two streams:
 // group g on stream g mod 2, its merge-only launches starting once group g - 1
@@ -334,10 +395,12 @@ void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStrea
     if (const char* e = std::getenv("RIPTIDE_AMD_CONE_FLAGS")) a.flags = (uint32_t)std::strtoul(e, nullptr, 0);
     a.blob = P.d_blob;
     const std::vector<Launch>& Ls = P.ex.launches;
-    if (P.ex.banks < 2 || P.ex.groups < 2) {
+    DeviceGuard dg(P.device);
+    const bool single = single_stream_forced();
+    if (single || P.ex.banks < 2 || P.ex.groups < 2) {
         bool multi = false;
         for (const Launch& L : Ls) multi = multi || L.smax != Ls.front().smax;
-        if (!multi) {
+        if (!multi || single) {
             for (const Launch& L : Ls) cone_launch(P, L, a, batch, s, true);
             return;
         }
@@ -351,7 +414,8 @@ void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStrea
         // (profiles/r04r_ab_*_bucketstreams.log); the cone time is then one
         // profiling record from the fork to the join.
         const uint32_t G = std::max<uint32_t>(P.ex.groups, 1);
-        SideSet* ss = P.take_side(2 * (size_t)G);
+        SideLease lease(P, 2 * (size_t)G, s);
+        SideSet* const ss = lease.ss;
         ProfRec r{};
         const bool prof = g_prof.on;
         if (prof) {
@@ -375,12 +439,13 @@ void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStrea
             for (const auto& kv : cells) if (kv.second > cells[mainb]) mainb = kv.first;
             ck(hipEventRecord(ss->ev[2 * g], s), "hipEventRecord");
             ck(hipStreamWaitEvent(ss->s2, ss->ev[2 * g], 0), "hipStreamWaitEvent");
+            lease.forked = true;
             for (; li < l1; ++li) cone_launch(P, Ls[li], a, batch, Ls[li].smax == mainb ? s : ss->s2, false);
             ck(hipEventRecord(ss->ev[2 * g + 1], ss->s2), "hipEventRecord");
             ck(hipStreamWaitEvent(s, ss->ev[2 * g + 1], 0), "hipStreamWaitEvent");
+            lease.forked = false;
         }
         if (li != Ls.size()) throw std::runtime_error("cone launches out of group order");
-        P.give_side(ss);
         if (prof) {
             ck(hipEventRecord(r.b, s), "hipEventRecord");
             std::lock_guard<std::mutex> lk(g_prof.mu);
@@ -389,7 +454,8 @@ void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStrea
         return;
     }
     const uint32_t G = P.ex.groups;
-    SideSet* ss = P.take_side(2 + G);
+    SideLease lease(P, 2 + (size_t)G, s);
+    SideSet* const ss = lease.ss;
     ProfRec r{};
     const bool prof = g_prof.on;
     if (prof) {
@@ -407,6 +473,7 @@ void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStrea
     hipEvent_t fork = ss->ev[0], join = ss->ev[1];
     ck(hipEventRecord(fork, s), "hipEventRecord");
     ck(hipStreamWaitEvent(ss->s2, fork, 0), "hipStreamWaitEvent");
+    lease.forked = true;
     size_t li = 0;
     for (uint32_t g = 0; g < G; ++g) {
         hipStream_t st = (g & 1u) ? ss->s2 : s;
@@ -418,7 +485,7 @@ void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStrea
     if (li != Ls.size()) throw std::runtime_error("cone launches out of group order");
     ck(hipEventRecord(join, ss->s2), "hipEventRecord");
     ck(hipStreamWaitEvent(s, join, 0), "hipStreamWaitEvent");
-    P.give_side(ss);
+    lease.forked = false;
     if (prof) {
         ck(hipEventRecord(r.b, s), "hipEventRecord");
         std::lock_guard<std::mutex> lk(g_prof.mu);

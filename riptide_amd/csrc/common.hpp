@@ -193,16 +193,16 @@ RT_HD inline int lds_row_capacity(uint32_t p, int smax)
 
 RT_HD inline int lds_row_capacity(uint32_t p) { return lds_row_capacity(p, merge_slots(p)); }
 
-// One FFA transform of a plan ((rung, bins) step of periodogram.hpp:223-269).
+// One FFA transform of a plan ((rung, bins) step of periodogram.hpp:153-199).
 struct FfaXform {
     uint32_t p;          // phase bins (= columns)
     uint32_t m;          // rows (= n / p)
-    uint32_t rows_eval;  // rows whose S/N is evaluated (periodogram.hpp:253)
+    uint32_t rows_eval;  // rows whose S/N is evaluated (periodogram.hpp:183)
     uint32_t rung;
     uint64_t src_off;    // float offset of the leaf rows in the per-trial leaf buffer
     uint64_t buf_off;    // float offset of the scratch rows in ping/pong
     uint64_t snr_row;    // first S/N output row (prefix sum of rows_eval)
-    float stdnoise;      // periodogram.hpp:251
+    float stdnoise;      // periodogram.hpp:181
     uint32_t pad;
 };
 static_assert(sizeof(FfaXform) == 48, "FfaXform layout");

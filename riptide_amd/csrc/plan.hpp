@@ -44,7 +44,7 @@ struct PgramPlan {
 // Ladder + steps (periodogram.hpp:135-183).  Arguments must be valid.
 void build_pgram_plan(const PgramParams& a, PgramPlan& plan);
 
-// periods[s] / foldbins[s] for all L rows (periodogram.hpp:260-264, in the form
+// periods[s] / foldbins[s] for all L rows (periodogram.hpp:190-194, in the form
 // the reference binary evaluates it: (B*B*tau) / fma(s, -1/(rows-1), B)).
 void fill_grid(const PgramPlan& plan, double* periods, uint32_t* foldbins);
 

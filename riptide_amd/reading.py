@@ -1,5 +1,5 @@
 """Readers of dedispersed time series files: SIGPROC .tim and PRESTO .inf/.dat
-(riptide/reading/sigproc.py:1-214, riptide/reading/presto.py:1-157,
+(riptide/reading/sigproc.py:1-197, riptide/reading/presto.py:1-149,
 riptide/metadata.py:54-106, riptide/time_series.py:283-362).
 
 Header parsing stays on the host; the bulk samples are read as raw bytes and,
@@ -90,7 +90,7 @@ def parse_float_coord(x):
 
 
 class SigprocHeader(dict):
-    """Header of a SIGPROC file (sigproc.py:162-214)."""
+    """Header of a SIGPROC file (sigproc.py:159-197)."""
 
     def __init__(self, fname, extra_keys=None):
         self._fname = os.path.abspath(fname)
@@ -254,7 +254,7 @@ def _sexagesimal(s):
 
 
 class PrestoInf(dict):
-    """PRESTO .inf metadata (presto.py:128-157)."""
+    """PRESTO .inf metadata (presto.py:124-149)."""
 
     def __init__(self, fname):
         self._fname = os.path.realpath(fname)

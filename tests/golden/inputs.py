@@ -170,6 +170,13 @@ def generated_series(tobs, tsamp, period, amplitude, ducy, generate_signal):
                                       stdnoise=1.0), dtype=np.float32)
 
 
+# The fused downsampling ladder's margin edge (kDsFusedMargin = 512 floats):
+# two rungs, f = 452.9 and 509.5125 (ceil(f) + 2 = 512, the largest window
+# the fused kernel stages), 16-17 bins.
+LADDER_EDGE_CASE = dict(n=1 << 20, tsamp=1e-3, pmin=452.9 * 1e-3 * 16, pmax=452.9 * 1e-3 * 16 * 1.125 ** 2 * 0.999,
+                        bmin=16, bmax=17, ducy_max=0.2)
+
+
 # ---------------------------------------------------------------- cfg5: rffa beam of SIGPROC files
 # BASELINE.json configs[4] at reduced trial count: 2^23-sample SIGPROC .tim
 # DM trials @ 64 us (537 s, "SUPERB-like"), refdm = 10 k, searched with

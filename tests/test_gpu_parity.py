@@ -4,6 +4,7 @@ oracle), trial grid, running median, dereddened series.  S/N: 1e-4 relative
 (BASELINE.json), scaled by max(|ref|, 1) since S/N is in units of sigma.
 """
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -330,7 +331,8 @@ def test_fused_ladder_matches_per_rung(monkeypatch):
     import torch
     from riptide_amd import engine
     cases = [inputs.PGRAM_CASES[1], dict(n=1 << 22, tsamp=256e-6, pmin=0.1, pmax=10.0, bmin=240, bmax=260,
-                                         ducy_max=0.05)]
+                                         ducy_max=0.05),
+             inputs.LADDER_EDGE_CASE]        # largest rung at the fused kernel's margin
     for case in cases:
         x = torch.from_numpy(np.random.RandomState(7).normal(size=(2, case["n"])).astype(np.float32)).cuda()
         outs = []
@@ -418,6 +420,62 @@ def test_bench_schedule_cfg2(rt, golden_full, monkeypatch):
     assert torch.equal(got, ref), "one-group schedule differs from the default grouping"
     periods, foldbins = one.grid()
     _check_full_snrs(rt, g, c, one, periods, foldbins, got[0].cpu().numpy())
+
+
+@pytest.mark.parametrize("name,budget", [("cfg2", "1536"), ("cfg4", None), ("cfg1", None), ("cfg3", "384")])
+def test_full_config_every_row(rt, oracle, golden_full, monkeypatch, name, budget):
+    """Every one of the L x W S/N values at full size (missing 3):
+    the golden input through the schedule bench.py times for the config,
+    compared element by element with the strict C oracle run on the same
+    dereddened, normalised series (periodogram.hpp:175-194; threaded, same
+    arithmetic per step) at the 2e-6 scaled tolerance of
+    test_periodogram_golden, and with the golden sampled rows / sums / peaks
+    of the reference build at 1e-4."""
+    import torch
+    from riptide_amd import engine
+    g = golden_full["configs"][name]
+    c = g["case"]
+    raw = inputs.full_input(c)
+    if sha(raw) != g["input_sha"]:
+        pytest.fail(f"input generator drifted on this host: input sha256 {sha(raw)} != golden {g['input_sha']}")
+    if budget:
+        monkeypatch.setenv("RIPTIDE_AMD_SCRATCH_MFLOATS", budget)
+    plan = engine.PeriodogramPlan.for_search(c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"],
+                                             ducy_max=c["ducy_max"])
+    x = engine.deredden_normalise(torch.from_numpy(raw).cuda(), int(round(4.0 / c["tsamp"])), 101)
+    snrs = plan.run(x, check=True).cpu().numpy()
+    periods, foldbins = plan.grid()
+    op, ofb, osnr = oracle.periodogram(x.cpu().numpy(), c["tsamp"], np.asarray(plan.widths, dtype=np.uint64),
+                                       c["pmin"], c["pmax"], c["bmin"], c["bmax"],
+                                       threads=min(16, os.cpu_count() or 1))
+    assert np.array_equal(periods, op) and np.array_equal(foldbins, ofb)
+    assert osnr.shape == snrs.shape == (g["length"], len(g["widths"]))
+    ok, msg = snr_close(snrs, osnr, rtol=2e-6)
+    assert ok, f"{name}: all {snrs.size} S/N values vs the strict oracle: {msg}"
+    _check_full_snrs(rt, g, c, plan, periods, foldbins, snrs)
+
+
+def test_single_stream_matches_two_streams_cfg2(rt, golden_full, monkeypatch):
+    """The two-stream slot-width chains (the default for plans with more than
+    one slot width, capi.cpp run_cone_launches) against every launch on the
+    caller's stream in plan order (RIPTIDE_AMD_SINGLE_STREAM=1): bit-identical
+    S/N on the benchmarked cfg2 schedule, golden input and its reverse."""
+    import torch
+    from riptide_amd import engine
+    g = golden_full["configs"]["cfg2"]
+    c = g["case"]
+    raw = inputs.full_input(c)
+    monkeypatch.setenv("RIPTIDE_AMD_SCRATCH_MFLOATS", "1536")
+    plan = engine.PeriodogramPlan.for_search(c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"],
+                                             ducy_max=c["ducy_max"])
+    d = torch.from_numpy(np.stack([raw, raw[::-1].copy()])).cuda()
+    x = engine.deredden_normalise(d, int(round(4.0 / c["tsamp"])), 101)
+    two = plan.run(x, check=True)
+    monkeypatch.setenv("RIPTIDE_AMD_SINGLE_STREAM", "1")
+    one = plan.run(x, check=True)
+    monkeypatch.delenv("RIPTIDE_AMD_SINGLE_STREAM")
+    torch.cuda.synchronize()
+    assert torch.equal(one, two), "single-stream schedule differs from the two-stream chains"
 
 
 @pytest.mark.parametrize("budget", ["384", "96"])
