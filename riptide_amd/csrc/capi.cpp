@@ -381,6 +381,18 @@ bool single_stream_forced()
     return e && e[0] == '1';
 }
 
+// Trials per cone workgroup (ConeArgs::trials_per_wg): one workgroup runs an
+// item for up to this many trials of the batch, its record, blob and roll
+// table loaded once.  RIPTIDE_AMD_TRIALS_PER_WG overrides the default.
+uint32_t cone_trials_per_wg()
+{
+    if (const char* e = std::getenv("RIPTIDE_AMD_TRIALS_PER_WG")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 1 && v <= 65535) return (uint32_t)v;
+    }
+    return kConeTrialsPerWg;
+}
+
 // Run all cone launches of an exec plan.  A plan with two scratch banks
 // (ExecPlan::banks) runs its transform groups co-scheduled on two streams:
 // group g on stream g mod 2, its merge-only launches starting once group g - 1
@@ -391,6 +403,7 @@ bool single_stream_forced()
 void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStream_t s)
 {
     a.batch = batch;
+    a.trials_per_wg = cone_trials_per_wg();
     a.flags = kConeDefaultFeatures;
     if (const char* e = std::getenv("RIPTIDE_AMD_CONE_FLAGS")) a.flags = (uint32_t)std::strtoul(e, nullptr, 0);
     a.blob = P.d_blob;

@@ -278,9 +278,22 @@ struct ConeArgs {
     int* error_flag;      // set non-zero if a work item violates the LDS budget
     const uint32_t* blob; // host-built tile-unit metadata (plan.hpp build_tile_blob); UnitDesc::pad = word offset
     unsigned long long* stamps;   // RT_STAMPS diagnostic builds only: per-phase cycles
-    uint32_t batch;       // trials: work unit u = (item u / batch, trial u % batch)
+    uint32_t batch;       // trials of the launch
     uint32_t flags;       // kCone* feature bits (A/B experiments; default all set)
+    // trials per workgroup (0 = 1): workgroup b runs item b / G for the trials
+    // (b % G) * T .. + T - 1 of the batch (G = ceil(batch / T)), one after
+    // the other in the same LDS: the item's record, blob (descriptors, slot
+    // tables) and roll table are loaded once for all T trials, and a merge-
+    // only unit issues the next trial's fill before storing the current one
+    uint32_t trials_per_wg;
 };
+constexpr uint32_t kConeTrialsPerWg = 16;  // default trials per workgroup (capi.cpp cone_trials_per_wg)
+// workgroups per item of a cone launch
+RT_HD inline uint32_t cone_trial_groups(uint32_t batch, uint32_t tpw)
+{
+    const uint32_t t = tpw ? tpw : 1u;
+    return (batch + t - 1) / t;
+}
 
 // Merge index of the FFA recursion (transforms.hpp:17-22): the reference build
 // evaluates (size_t)(k * s + 0.5f) with k = (child_rows - 1.0f) / (rows - 1.0f)

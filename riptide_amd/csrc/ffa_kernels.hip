@@ -329,6 +329,8 @@ struct UnitCtx {
     int nruns, entries, nb;   // blob header counts
     const uint32_t* aux;      // the blob's LDS part in LDS
     const uint32_t* aux0;     // the workgroup's metadata area (roll table at kLut4Off)
+    uint4 sv;                 // tile units: this wave's DMA segments (lane i: segment wave + 8i), the
+    int mine;                 // same for every trial; `mine` of them
 };
 
 __device__ __forceinline__ int rows_at(const UnitCtx& C, int l)
@@ -371,20 +373,81 @@ __device__ __forceinline__ void dma_run(__amdgpu_buffer_rsrc_t rs, uint32_t goff
     }
 }
 
-// Starts unit (item, trial): its view, and (dma) the LDS DMA of its bottom
-// level into `buf` and, for a tile unit, of its blob into `aux`.  Nothing is
-// waited for: the caller waits (vmcnt) and barriers before reading LDS.
-// `ok` = the kernel instance can run the unit (the host validates every
-// schedule, validate_exec_plan; this guards the error flag): LDS buffer and
-// register rows, the metadata area, rows of exactly SMAX slots for SMAX <= 5
-// (unmasked full slots; kPack2: the p <= 32 rows).
-template <int SMAX, int RW>
-__device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t u, uint32_t* aux, float* buf, int tid,
-                                              bool dma, bool& ok, unsigned long long* ts = nullptr)
+// Source block (the transform's rows in the leaf buffer or ping / pong) of a
+// unit's bottom level for `trial`, as a buffer resource over the block.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t unit_src(const ConeArgs& a, const UnitView& U, int trial)
+{
+    const float* src;
+    if (U.src == kSelLeaves) src = a.leaves + (uint64_t)trial * a.leaves_stride + U.src_off;
+    else src = (U.src == kSelPing ? a.ping : a.pong) + (uint64_t)trial * a.buf_stride + U.buf_off;
+    // transform blocks start 16-byte aligned and are padded to 4 floats
+    return buffer_rsrc(src, (((uint32_t)U.m * (uint32_t)U.p + 3u) & ~3u) * 4u);
+}
+
+// Issues the LDS DMA of a unit's bottom level for `trial` into `buf` (a whole
+// unit: one run of 16-byte chunks; a tile unit: the host-built DMA segments,
+// one vector load, lane i of wave w holding segment w + 8i) and, with
+// `blob_too`, the blob's LDS part (header, descriptors, bottom-row offsets,
+// slot tables) into the metadata area.  Nothing is waited for.
+template <int SMAX>
+__device__ __forceinline__ void unit_fill(const ConeArgs& a, const UnitCtx& C, int trial, float* buf, int tid,
+                                          bool blob_too)
 {
     const int lane = tid & 63, wave = tid >> 6;
+    const UnitView& U = C.U;
+    const int p = U.p;
+    const __amdgpu_buffer_rsrc_t rs = unit_src(a, U, trial);
+    if (!C.table) {
+        const int nch = (U.node_size * p + C.al + 3) >> 2;
+        dma_run(rs, ((uint32_t)U.node_start * (uint32_t)p - (uint32_t)C.al) * 4u, nch, buf, wave, kConeWaves, lane);
+        return;
+    }
+    const int words = U.run_off;   // the LDS part: header .. slot tables
+    // the wave's DMA segments (unit_segments, loaded once per workgroup)
+    const uint4 sv = C.sv;
+    const int mine = C.mine;
+    if (blob_too && wave == kConeWaves - 1) {
+        const __amdgpu_buffer_rsrc_t rb = buffer_rsrc(a.blob + U.blob, (uint32_t)words * 4u);
+        dma_run(rb, 0u, words >> 2, (float*)const_cast<uint32_t*>(C.aux), 0, 1, lane);
+    }
+    for (int i = 0; i < mine; ++i) {
+        const int c0 = __builtin_amdgcn_readlane((int)sv.x, i);
+        const int n = __builtin_amdgcn_readlane((int)sv.y, i);
+        const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)sv.z, i);
+        if (lane < n && 4 * (c0 + n) <= kLdsBufFloats && !(a.flags & kConeDiagNoFill))
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(buf + 4 * c0), 16,
+                                                     (int)((g + (uint32_t)lane) * 16u), 0, 0, kFillCpol);
+    }
+}
+
+// The wave's DMA segments of a tile unit: wave w issues segments w, w + 8,
+// ...; its lane i holds segment w + 8i (one coalesced vector load; wave-major
+// table, build_tile_blob: the wave's segments are consecutive).  Trial-
+// independent: kept in registers for every trial of the workgroup.
+__device__ __forceinline__ void unit_segments(const ConeArgs& a, UnitCtx& C, int tid)
+{
+    const int lane = tid & 63, wave = tid >> 6;
+    const uint4* const segs = reinterpret_cast<const uint4*>(a.blob + C.U.blob + C.U.run_off);
+    C.mine = uni(C.nruns > wave ? (C.nruns - wave + kConeWaves - 1) / kConeWaves : 0);
+    C.sv = make_uint4(0u, 0u, 0u, 0u);
+    const int K = (C.nruns + kConeWaves - 1) / kConeWaves;
+    if (lane < C.mine) C.sv = segs[wave * K + lane];
+}
+
+// Starts the unit of `item` at trial `trial`: its view (one scalar load of
+// its UnitDesc) and, with `dma`, the LDS DMA of its blob into `aux` and of its
+// bottom level into `buf` (unit_fill).  Nothing is waited for: the caller
+// waits (vmcnt) and barriers before reading LDS.  `ok` = the kernel instance
+// can run the unit (the host validates every schedule, validate_exec_plan;
+// this guards the error flag): LDS buffer and register rows, the metadata
+// area, rows of exactly SMAX slots for SMAX <= 5 (unmasked full slots;
+// kPack2: the p <= 32 rows).
+template <int SMAX, int RW>
+__device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t item, uint32_t trial, uint32_t* aux,
+                                              float* buf, int tid, bool dma, bool& ok, unsigned long long* ts = nullptr)
+{
     UnitCtx C;
-    C.U = unit_view(a, (int)(u / a.batch), (int)(u % a.batch));
+    C.U = unit_view(a, (int)item, (int)trial);
     const UnitView& U = C.U;
 #ifdef RT_STAMPS
     if (ts) ts[0] = __builtin_amdgcn_s_memtime() + (U.p & 0);
@@ -398,29 +461,20 @@ __device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t u, uin
     ok = U.levels <= kMaxLevels && p > 0 &&
          ((SMAX <= 5 || SMAX == kPack2) ? slots == SMAX : (slots <= SMAX && slots != kPack2));
     const int cap = min(lds_row_capacity((uint32_t)p, SMAX), kConeWaves * RW * row_pack(SMAX));
-    const float* src;
-    if (U.src == kSelLeaves) src = a.leaves + (uint64_t)U.trial * a.leaves_stride + U.src_off;
-    else src = (U.src == kSelPing ? a.ping : a.pong) + (uint64_t)U.trial * a.buf_stride + U.buf_off;
-    // transform blocks start 16-byte aligned and are padded to 4 floats
-    const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(src, (((uint32_t)U.m * (uint32_t)p + 3u) & ~3u) * 4u);
     if (!C.table) {
-        ok = ok && SMAX != kPack2;    // short-row units always carry a blob
+        // short-row units always carry a blob, 4/5-slot units slot tables
+        ok = ok && SMAX != kPack2 && (!resolved_slots(SMAX) || U.levels == 0);
         C.al = (int)(((uint32_t)U.node_start * (uint32_t)p) & 3u);
         C.slots = false;
         C.nruns = C.entries = C.nb = 0;
         const int nch = (U.node_size * p + C.al + 3) >> 2;
         ok = ok && !C.tile && U.node_size <= cap && 4 * nch <= kLdsBufFloats;
-#ifdef RT_STAMPS
-        if (ts) ts[1] = __builtin_amdgcn_s_memtime();
-#endif
-        if (ok && dma)
-            dma_run(rs, ((uint32_t)U.node_start * (uint32_t)p - (uint32_t)C.al) * 4u, nch, buf, wave, kConeWaves, lane);
     } else {
         C.al = 0;
         // the blob's header counts come with the view (UnitDesc); its DMA
-        // runs with one vector load (lane i: run i) -- the unit's DMA is
-        // issued two memory round trips after the workgroup starts (a scalar
-        // load per run took ~10K cycles for a 16-run tile)
+        // runs with one vector load -- the unit's DMA is issued two memory
+        // round trips after the workgroup starts (a scalar load per run took
+        // ~10K cycles for a 16-run tile)
         C.nruns = U.nruns;
         C.entries = U.entries;
         C.nb = U.nb;
@@ -436,32 +490,19 @@ __device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t u, uin
             ok = ok && C.nb <= cap && C.entries <= kDescEntries && words <= kAuxWords;
             // the 4-slot roll table lies past the blob's LDS part
             if (SMAX == 4 && C.slots) ok = ok && words <= kLut4Off;
+            // the 4/5-slot instances run row-slot steps only (merge_levels)
+            if (resolved_slots(SMAX)) ok = ok && (U.levels == 0 || (C.slots && (a.flags & kConeFuse2)));
         }
         ok = ok && words >= kBlobHeader + C.entries + C.nb && C.nruns <= 64 * kConeWaves && (words & 3) == 0;
+    }
 #ifdef RT_STAMPS
-        if (ts) ts[1] = __builtin_amdgcn_s_memtime() + (ok ? 0 : 0);
+    if (ts) ts[1] = __builtin_amdgcn_s_memtime() + (ok ? 0 : 0);
 #endif
-        if (ok && dma) {
-            // DMA segments: wave w issues segments w, w + 8, ...; its lane i
-            // holds segment w + 8i (one coalesced vector load)
-            const uint4* const segs = reinterpret_cast<const uint4*>(a.blob + U.blob + words);
-            const int mine = uni(C.nruns > wave ? (C.nruns - wave + kConeWaves - 1) / kConeWaves : 0);
-            uint4 sv = make_uint4(0u, 0u, 0u, 0u);
-            // wave-major table (build_tile_blob): the wave's segments are consecutive
-            const int K = (C.nruns + kConeWaves - 1) / kConeWaves;
-            if (lane < mine) sv = segs[wave * K + lane];
-            // the blob's LDS part: the last wave
-            const __amdgpu_buffer_rsrc_t rb = buffer_rsrc(a.blob + U.blob, (uint32_t)words * 4u);
-            if (wave == kConeWaves - 1) dma_run(rb, 0u, words >> 2, (float*)const_cast<uint32_t*>(C.aux), 0, 1, lane);
-            for (int i = 0; i < mine; ++i) {
-                const int c0 = __builtin_amdgcn_readlane((int)sv.x, i);
-                const int n = __builtin_amdgcn_readlane((int)sv.y, i);
-                const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)sv.z, i);
-                if (lane < n && 4 * (c0 + n) <= kLdsBufFloats && !(a.flags & kConeDiagNoFill))
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(buf + 4 * c0),
-                                                             16, (int)((g + (uint32_t)lane) * 16u), 0, 0, kFillCpol);
-            }
-        }
+    C.sv = make_uint4(0u, 0u, 0u, 0u);
+    C.mine = 0;
+    if (ok && dma) {
+        if (C.table) unit_segments(a, C, tid);
+        unit_fill<SMAX>(a, C, (int)trial, buf, tid, true);
     }
 #ifdef RT_STAMPS
     if (ts) ts[2] = __builtin_amdgcn_s_memtime();
@@ -1432,10 +1473,13 @@ __device__ __forceinline__ void put_tasks(float* base, int q, const float (&v)[k
 // Each level's outputs are staged in registers between two barriers, then
 // written back.  With `st` set (a non-final pass), the output level goes from
 // the staging registers straight to global memory instead of back into LDS.
-template <int SMAX, int RW>
+// pre_store(): called by every wave after the last merge step's LDS reads
+// and before its output level is stored from registers (st): the level
+// buffer is then free for the next trial's fill.
+template <int SMAX, int RW, class PreStore>
 __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int p, int L, int tid, bool st,
                                              __amdgpu_buffer_rsrc_t rs, uint32_t st_o0, uint32_t flags, float* dummy,
-                                             int qout)
+                                             int qout, PreStore&& pre_store)
 {
     const int lane = tid & 63, wave = tid >> 6;
     const bool tile = C.tile;
@@ -1479,6 +1523,7 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
                 else step(IntC<0>{});
                 l = lo - 1;
                 if (lo == 0 && st) {
+                    pre_store();
                     put_tasks<true, 0>(base, qs, v, p, tid, nrows, rs, st_o0);
                     return;
                 }
@@ -1512,6 +1557,7 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
             }
             l = lo - 1;
             if (lo == 0 && st) {
+                pre_store();
                 store_rows_lanes<RW>(v, p, lane, wave, nrows, rs, st_o0);
                 return;
             }
@@ -1522,7 +1568,11 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
         return;
     }
     if constexpr (SMAX <= 5) {
-        if (C.slots && fuse) {
+        // the 4/5-slot instances (p = 193-320) run only row-slot steps: every
+        // unit of theirs carries slot tables (validate_exec_plan; unit_begin
+        // refuses a unit without them), so the dense per-level paths below are
+        // compiled out of these, the hottest instances
+        if (resolved_slots(SMAX) || (C.slots && fuse)) {
             // row-slot steps (the host's slot tables follow this step order)
             for (int l = L - 1; l >= 0;) {
                 const bool two = l >= 1 && (tile || (node_size >> l) >= 2);
@@ -1537,6 +1587,7 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
                 else merge_step_slots<SMAX, RW, false>(C, src, p, lo, lane, wave, v, lo_src, sw, nq);
                 l = lo - 1;
                 if (lo == 0 && st) {
+                    pre_store();
                     store_rows_slots<SMAX, RW>(v, p, lane, sw, nq, rs, st_o0);
                     return;
                 }
@@ -1549,6 +1600,7 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
             return;
         }
     }
+    if constexpr (!resolved_slots(SMAX)) {
     for (int l = L - 1; l >= 0;) {
         // size-1 nodes exist at depth l only in whole units with node_size >> l < 2
         const bool two = fuse && l >= 1 && (tile || (node_size >> l) >= 2);
@@ -1569,6 +1621,7 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
             merge_level_dense<S, RW, false>(C, src, p, l, lane, wave, nr, v, lo_src);
         l = lo - 1;
         if (lo == 0 && st) {
+            pre_store();
             store_rows<S, RW>(v, p, lane, wave, nr, rs, st_o0);
             return;
         }
@@ -1577,6 +1630,7 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
             write_rows<S, RW>(base, dummy, v, p, lane, wave, nr);
         }
         if (!(flags & kConeDiagNoBarrier)) lds_barrier();
+    }
     }
 }
 
@@ -2117,6 +2171,9 @@ template <int SMAX, bool WIDE = false>
 __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& U, float* data, int q, const int* wl,
                                              int nrows, int tid, float* whb, unsigned long long* tl)
 {
+    // an opaque thread index: nothing lane-derived of the S/N is hoisted out
+    // of the kernel's trial loop into registers live across the merge
+    asm volatile("" : "+v"(tid));
     const int lane = tid & 63, wave = tid >> 6;
     const int p = U.p;
     const int nev = (int)min((int64_t)nrows, (int64_t)U.rows_eval - (int64_t)U.s0);
@@ -2244,6 +2301,14 @@ __device__ __forceinline__ void snr_epilogue(const ConeArgs& a, const UnitView& 
 // WIDE: final units whose S/N takes the widths past its register window as
 // plain LDS windows (snr_wide_ok; a separate instantiation, so the plans
 // without such widths run code without it)
+// instances whose workgroups run several trials of an item (ConeArgs::
+// trials_per_wg); the others one trial each
+#ifdef RT_NO_TRIAL_LOOP
+template <int SMAX> constexpr bool kTrialLoop = false;   // A/B build: one trial per workgroup everywhere
+#else
+template <int SMAX> constexpr bool kTrialLoop = SMAX >= 4;
+#endif
+
 template <int SMAX, int RWT, bool WIDE, bool SNR>
 __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(ConeArgs a)
 {
@@ -2257,13 +2322,20 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
 
     const int tid = threadIdx.x;
 #ifdef RT_STAMPS
-    const unsigned long long t_entry = __builtin_amdgcn_s_memtime();
-    const unsigned long long r_entry = __builtin_amdgcn_s_memrealtime();
+    unsigned long long t_entry = __builtin_amdgcn_s_memtime();
+    unsigned long long r_entry = __builtin_amdgcn_s_memrealtime();
     unsigned long long t_begin[3] = {};
 #endif
-    const uint32_t total = a.num_items * a.batch;
+    // workgroup -> (item, its trials t0 .. t0 + tn - 1); the 1-3-slot
+    // instances (p = 33-192, no BASELINE config) run one trial per workgroup
+    // (launch_cone): their trial loop would spill
+    const uint32_t tpw = (kTrialLoop<SMAX> && a.trials_per_wg) ? a.trials_per_wg : 1u;
+    const uint32_t groups = cone_trial_groups(a.batch, tpw);
+    const uint32_t total = a.num_items * groups;
     if (blockIdx.x >= total) return;
-    const uint32_t u = blockIdx.x;
+    const uint32_t item = blockIdx.x / groups;
+    const uint32_t t0 = (blockIdx.x - item * groups) * tpw;
+    const int tn = (int)min(tpw, a.batch - t0);
     if (tid < (int)a.num_widths) wl[tid] = (int)a.widths[tid];   // visible after the first barrier
     if (tid == 0) {
         uint32_t wm = 0;
@@ -2273,11 +2345,11 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
     const bool dma = !(a.flags & kConeDiagNoLand);
     bool ok;
 #ifdef RT_STAMPS
-    const UnitCtx C = unit_begin<SMAX, RW>(a, u, aux, data, tid, dma, ok, t_begin);
+    UnitCtx C = unit_begin<SMAX, RW>(a, item, t0, aux, data, tid, dma, ok, t_begin);
     unsigned long long tl[kStampMarks] = {};
     tl[0] = __builtin_amdgcn_s_memtime();
 #else
-    const UnitCtx C = unit_begin<SMAX, RW>(a, u, aux, data, tid, dma, ok);
+    UnitCtx C = unit_begin<SMAX, RW>(a, item, t0, aux, data, tid, dma, ok);
 #endif
     const UnitView& U = C.U;
     const int p = U.p;
@@ -2303,57 +2375,77 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
     RT_MARK(2);
     if (!ok) {
         if (tid == 0 && a.error_flag) atomicOr(a.error_flag, 1);
-    } else {
-        // merge levels, deepest first; a non-final pass stores its output
-        // level straight from registers (st), a final pass keeps it in LDS
-        // for the S/N epilogue
-        constexpr bool st = !SNR;
-        const bool st_regs = st && (a.flags & kConeStoreFromRegs);
-        const float* dst = (U.dst == kSelPing ? a.ping : a.pong) + (uint64_t)U.trial * a.buf_stride + U.buf_off;
+        return;
+    }
+    // merge levels, deepest first; a non-final pass stores its output level
+    // straight from registers (st), a final pass keeps it in LDS for the S/N
+    // epilogue
+    constexpr bool st = !SNR;
+    const bool st_regs = st && (a.flags & kConeStoreFromRegs);
+    const uint32_t o0 = (uint32_t)(U.node_start + U.s0) * (uint32_t)p * 4u;
+    const int n0 = rows_at(C, 0);
+    // a final pass's output level at a row stride = 16 (mod 32): the S/N
+    // epilogue's lane groups (two rows of 16 lanes per 32-lane LDS group, odd
+    // chunk strides) then read and write on distinct banks (at stride p they
+    // collided on up to 10 of 32 banks)
+    int qout = p;
+    // short rows keep their blob's LDS part at the end of the level buffer,
+    // which a final pass's output level (at the S/N stride) and its S/N's
+    // dummy words may overwrite: every trial's fill then re-DMAs it
+    const bool blob_clobbered = SMAX == kPack2 && SNR;
+    // short rows in (row, segment) tasks: every level above the fill at the
+    // odd stride pack_stride(p)
+    if constexpr (SMAX == kPack2) {
+        if (L > 0) qout = pack_stride(p);
+        // a final pass's output level at the short-row S/N stride where the
+        // unit's rows fit (over the blob: the blob is dead once the last
+        // merge step has read its table, a barrier before the level's
+        // write-back)
+        if (SNR && L > 0 && p >= kPackSeg && (a.flags & kConeSnrStride)) {
+            const int qf = snr_short_stride(p);
+            if (n0 * qf <= kLdsDataFloats) qout = qf;
+        }
+    }
+    if constexpr (SMAX <= 5 && SMAX != kPack2) {
+        // = 16 (mod 32) and >= p + kSnrMaxChunk (room for the S/N's whole-
+        // chunk prefix writes and its wrapped prefix extension), else >=
+        // p + kSnrWin (the extension only)
+        const int qa = p + kSnrMaxChunk + ((16 - ((p + kSnrMaxChunk) & 31)) & 31);
+        const int qb = p + kSnrWin + ((16 - ((p + kSnrWin) & 31)) & 31);
+        if (!st && L > 0 && C.slots && (a.flags & kConeFuse2) && (a.flags & kConeSnrStride)) {
+            qout = n0 * qa <= kLdsDataFloats ? qa : (n0 * qb <= kLdsDataFloats ? qb : p);
+            // widths past the register window: a stride with room for their
+            // plain-LDS windows (snr_wide_stride), = 16 (mod 32) where that
+            // fits too
+            const int wmax = wl[kMaxWidths];
+            if (WIDE && snr_group(p) == 16 && wmax > kSnrWin && wmax < p) {
+                const int qw = snr_wide_stride(p, wmax);
+                const int qwp = qw + ((16 - (qw & 31)) & 31);
+                if (n0 * qwp <= kLdsDataFloats) qout = qwp;
+                else if (n0 * qw <= kLdsDataFloats) qout = qw;
+            }
+        }
+    }
+    // the trials of this workgroup, one after the other: trial k's level
+    // buffer is free once its last merge step has read it (merge-only units
+    // store that step from registers: the next trial's fill is issued before
+    // those stores) or once its S/N has read it (final units)
+    for (int k = 0;;) {
+        const int trial = C.U.trial;
+        const float* dst = (U.dst == kSelPing ? a.ping : a.pong) + (uint64_t)trial * a.buf_stride + U.buf_off;
         const __amdgpu_buffer_rsrc_t rs = buffer_rsrc(dst, (((uint32_t)U.m * (uint32_t)p + 3u) & ~3u) * 4u);
-        const uint32_t o0 = (uint32_t)(U.node_start + U.s0) * (uint32_t)p * 4u;
-        const int n0 = rows_at(C, 0);
-        // a final pass's output level at a row stride = 16 (mod 32): the
-        // S/N epilogue's lane groups (two rows of 16 lanes per 32-lane LDS
-        // group, odd chunk strides) then read and write on distinct banks
-        // (at stride p they collided on up to 10 of 32 banks)
-        int qout = p;
-        // short rows in (row, segment) tasks: every level above the fill at
-        // the odd stride pack_stride(p)
-        if constexpr (SMAX == kPack2) {
-            if (L > 0) qout = pack_stride(p);
-            // a final pass's output level at the short-row S/N stride where
-            // the unit's rows fit (over the blob: the blob is dead once the
-            // last merge step has read its table, a barrier before the
-            // level's write-back)
-            if (SNR && L > 0 && p >= kPackSeg && (a.flags & kConeSnrStride)) {
-                const int qf = snr_short_stride(p);
-                if (n0 * qf <= kLdsDataFloats) qout = qf;
+        const bool more = k + 1 < tn;
+        bool next_issued = false;
+        auto fill_next = [&]() {
+            if (more) {
+                lds_barrier();           // every wave is past its last read of the level buffer
+                if (dma) unit_fill<SMAX>(a, C, trial + 1, buf, tid, blob_clobbered);
             }
-        }
-        if constexpr (SMAX <= 5 && SMAX != kPack2) {
-            // = 16 (mod 32) and >= p + kSnrMaxChunk (room for the S/N's whole-
-            // chunk prefix writes and its wrapped prefix extension), else >=
-            // p + kSnrWin (the extension only)
-            const int qa = p + kSnrMaxChunk + ((16 - ((p + kSnrMaxChunk) & 31)) & 31);
-            const int qb = p + kSnrWin + ((16 - ((p + kSnrWin) & 31)) & 31);
-            if (!st && L > 0 && C.slots && (a.flags & kConeFuse2) && (a.flags & kConeSnrStride)) {
-                qout = n0 * qa <= kLdsDataFloats ? qa : (n0 * qb <= kLdsDataFloats ? qb : p);
-                // widths past the register window: a stride with room for
-                // their plain-LDS windows (snr_wide_stride), = 16 (mod 32)
-                // where that fits too
-                const int wmax = wl[kMaxWidths];
-                if (WIDE && snr_group(p) == 16 && wmax > kSnrWin && wmax < p) {
-                    const int qw = snr_wide_stride(p, wmax);
-                    const int qwp = qw + ((16 - (qw & 31)) & 31);
-                    if (n0 * qwp <= kLdsDataFloats) qout = qwp;
-                    else if (n0 * qw <= kLdsDataFloats) qout = qw;
-                }
-            }
-        }
+            next_issued = true;
+        };
         if (L > 0 && !(a.flags & kConeDiagNoMerge))
             merge_levels<SMAX, RW>(C, buf, p, L, tid, st_regs, rs, o0, a.flags, buf + kLdsBufFloats + 4 + (tid & 63),
-                                   qout);
+                                   qout, fill_next);
         RT_MARK(3);
         // the output level: dense rows from the buffer start, or (no merge
         // level) the single bottom row where the DMA left it
@@ -2368,36 +2460,54 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
             }
         } else if constexpr (SNR) {
 #ifdef RT_STAMPS
-            if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(a, U, obase, qout, wl, n0, tid, whb, tl);
+            if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(a, C.U, obase, qout, wl, n0, tid, whb, tl);
 #else
-            if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(a, U, obase, qout, wl, n0, tid, whb, nullptr);
+            if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(a, C.U, obase, qout, wl, n0, tid, whb, nullptr);
 #endif
         }
-    }
 #ifdef RT_STAMPS
-    lds_barrier();
-    RT_MARK(4);
-    tl[5] = t_entry;
-    tl[11] = t_begin[0];
-    tl[12] = t_begin[1];
-    tl[13] = t_begin[2];
-    RT_MARK(6);
-    tl[14] = r_entry;
-    tl[15] = __builtin_amdgcn_s_memrealtime();
-    if (tid == 0 && a.stamps) {
-        unsigned long long* e = a.stamps + (uint64_t)kStampRecWords * (uint64_t)u;
-        const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));     // HW_REG_HW_ID
-        const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11));   // HW_REG_XCC_ID
-        e[0] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+        lds_barrier();
+        RT_MARK(4);
+        tl[5] = t_entry;
+        tl[11] = t_begin[0];
+        tl[12] = t_begin[1];
+        tl[13] = t_begin[2];
+        RT_MARK(6);
+        tl[14] = r_entry;
+        tl[15] = __builtin_amdgcn_s_memrealtime();
+        if (tid == 0 && a.stamps) {
+            unsigned long long* e = a.stamps + (uint64_t)kStampRecWords * ((uint64_t)item * a.batch + (uint32_t)trial);
+            const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));     // HW_REG_HW_ID
+            const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11));   // HW_REG_XCC_ID
+            e[0] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
 #pragma unroll
-        for (int i = 0; i < kStampMarks; ++i) e[1 + i] = tl[i];
-        e[1 + kStampMarks] = (unsigned long long)p | ((unsigned long long)L << 16) |
-                             ((unsigned long long)U.mode << 24) | ((unsigned long long)rows_at(C, 0) << 32) |
-                             ((unsigned long long)(U.dst == kSelSnr) << 48);
-    }
+            for (int i = 0; i < kStampMarks; ++i) e[1 + i] = tl[i];
+            e[1 + kStampMarks] = (unsigned long long)p | ((unsigned long long)L << 16) |
+                                 ((unsigned long long)U.mode << 24) | ((unsigned long long)rows_at(C, 0) << 32) |
+                                 ((unsigned long long)(U.dst == kSelSnr) << 48);
+        }
 #endif
-    // every DMA was waited for at the unit start, and the unit's global
-    // stores need no wait before the end of the program
+        if (!kTrialLoop<SMAX> || !more) break;
+        // final units (and merge-only units not stored from registers): the
+        // next trial's fill once every wave is done with the level buffer
+        if (!next_issued) fill_next();
+        ++k;
+        C.U.trial = trial + 1;
+#ifdef RT_STAMPS
+        t_entry = __builtin_amdgcn_s_memtime();
+        r_entry = __builtin_amdgcn_s_memrealtime();
+        t_begin[0] = t_begin[1] = t_begin[2] = t_entry;
+        tl[0] = t_entry;
+#endif
+        // the next trial's fill (and this trial's stores, which count in the
+        // same in-order counter) landed; the barrier publishes every wave's
+        __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)
+        lds_barrier();
+        RT_MARK(1);
+        RT_MARK(2);
+    }
+    // every DMA was waited for before its trial, and the stores need no wait
+    // before the end of the program
 }
 
 // One workgroup per unit: the hardware dispatcher keeps both of a CU's
@@ -2419,10 +2529,16 @@ static hipError_t launch_kind(const ConeArgs& args, dim3 g, dim3 b, bool wide_sn
     return hipSuccess;
 }
 
-hipError_t launch_cone(const ConeArgs& args, uint32_t smax, uint32_t rw, bool wide_snr, bool snr, hipStream_t s)
+hipError_t launch_cone(const ConeArgs& args_in, uint32_t smax, uint32_t rw, bool wide_snr, bool snr, hipStream_t s)
 {
-    if (!args.num_items || !args.batch) return hipSuccess;
-    const uint64_t total = (uint64_t)args.num_items * args.batch;
+    if (!args_in.num_items || !args_in.batch) return hipSuccess;
+    ConeArgs args = args_in;
+#ifdef RT_NO_TRIAL_LOOP
+    args.trials_per_wg = 1;
+#else
+    if (smax < 4) args.trials_per_wg = 1;    // kTrialLoop: one trial per workgroup
+#endif
+    const uint64_t total = (uint64_t)args.num_items * cone_trial_groups(args.batch, args.trials_per_wg);
     if (total > 0xFFFFFFFFull) return hipErrorInvalidValue;
     const dim3 g((uint32_t)total), b(kConeBlock);
     hipError_t e = hipErrorInvalidValue;

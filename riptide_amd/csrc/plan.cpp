@@ -964,6 +964,11 @@ void validate_exec_plan(const ExecPlan& ex, bool snr_epilogue)
             } else if (it.mode == kModeTile && (need.entries > kDescEntries || it.pad == kNoBlob)) {
                 throw std::runtime_error("schedule: tile descriptor table exceeds its LDS area");
             }
+            // the 4/5-slot instances run only row-slot steps (ffa_kernels.hip
+            // merge_levels): every unit with a merge level has its slot tables
+            if (resolved_slots((int)L.smax) && it.levels > 0 &&
+                (it.pad == kNoBlob || ex.blob[it.pad + kHdrSlotWords] == 0))
+                throw std::runtime_error("schedule: 4/5-slot unit without row-slot tables");
             // the launch's kernel instance is the unit's kind (final: fused S/N)
             if ((it.dst == kSelSnr) != (L.snr != 0)) throw std::runtime_error("schedule: unit in a launch of the other kind");
             if (L.wide_snr && !L.snr) throw std::runtime_error("schedule: wide S/N on a merge-only launch");
