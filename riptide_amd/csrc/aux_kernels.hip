@@ -4,6 +4,8 @@
 // kernel-API helpers (rollback, fused_rollback_add, circular_prefix_sum).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <cmath>
 
 #include "common.hpp"
@@ -140,6 +142,105 @@ __global__ __launch_bounds__(kRmedTile) void rmed_small_kernel(const float* __re
     out[i] = res;
 }
 
+// Small windows, kRmedRun consecutive outputs per thread: the first by the
+// counting search of rmed_small_kernel, each next one from the previous
+// median m (one sample leaves the window, one enters, so the median moves by
+// at most one place in sorted order): m itself if its rank still fits, else
+// the largest window value below m or the smallest above it, each verified
+// by its rank; any miss (NaN data) takes the full search.  The value returned
+// is then the window's first element equal to the median (the element the
+// full search returns: the median value is unique, and of equal values it
+// picks the first in window order -- +0.0 / -0.0 included).  kRmedRun is
+// odd, so the 64 lanes' LDS reads (stride kRmedRun) land on distinct banks.
+constexpr int kRmedRun = 7;
+
+__device__ __forceinline__ void rank_of(const float* win, int width, float v, int& less, int& leq)
+{
+    // four independent counter pairs: the window's LDS reads go out four at
+    // a time instead of one read-compare-add chain
+    int l0 = 0, l1 = 0, l2 = 0, l3 = 0, q0 = 0, q1 = 0, q2 = 0, q3 = 0;
+    int k = 0;
+    for (; k + 4 <= width; k += 4) {
+        const float u0 = win[k], u1 = win[k + 1], u2 = win[k + 2], u3 = win[k + 3];
+        l0 += u0 < v; q0 += u0 <= v;
+        l1 += u1 < v; q1 += u1 <= v;
+        l2 += u2 < v; q2 += u2 <= v;
+        l3 += u3 < v; q3 += u3 <= v;
+    }
+    for (; k < width; ++k) {
+        const float u = win[k];
+        l0 += u < v;
+        q0 += u <= v;
+    }
+    less = (l0 + l1) + (l2 + l3);
+    leq = (q0 + q1) + (q2 + q3);
+}
+
+__global__ __launch_bounds__(kRmedTile) void rmed_run_kernel(const float* __restrict__ x, uint64_t n, int width,
+                                                             float* __restrict__ out, uint64_t x_stride,
+                                                             uint64_t out_stride)
+{
+    __shared__ float span[kRmedTile * kRmedRun + kRmedSmallMax];
+    x += (uint64_t)blockIdx.y * x_stride;
+    out += (uint64_t)blockIdx.y * out_stride;
+    const int half = width / 2;
+    const int64_t i0 = (int64_t)blockIdx.x * (kRmedTile * kRmedRun);
+    for (int k = threadIdx.x; k < kRmedTile * kRmedRun + width - 1; k += kRmedTile) {
+        int64_t idx = i0 - half + k;
+        idx = idx < 0 ? 0 : (idx >= (int64_t)n ? (int64_t)n - 1 : idx);
+        span[k] = x[idx];
+    }
+    __syncthreads();
+    const int64_t ib = i0 + (int64_t)threadIdx.x * kRmedRun;
+    float m = 0.0f;
+    bool have = false;
+    for (int r = 0; r < kRmedRun; ++r) {
+        if (ib + r >= (int64_t)n) return;
+        const float* win = span + threadIdx.x * kRmedRun + r;
+        bool found = false;
+        if (have) {
+            int less, leq;
+            rank_of(win, width, m, less, leq);
+            if (less <= half && half < leq) {
+                found = true;
+            } else if (less > half || leq <= half) {
+                // the neighbour in sorted order: max below m or min above it
+                const bool down = less > half;
+                float c = down ? -INFINITY : INFINITY;
+                for (int k = 0; k < width; ++k) {
+                    const float u = win[k];
+                    c = down ? (u < m && u > c ? u : c) : (u > m && u < c ? u : c);
+                }
+                rank_of(win, width, c, less, leq);
+                if (less <= half && half < leq) {
+                    m = c;
+                    found = true;
+                }
+            }
+            if (found) {
+                // the window's first element equal to the median
+                int k = 0;
+                while (k < width && !(win[k] == m)) ++k;
+                if (k < width) m = win[k];
+                else found = false;
+            }
+        }
+        if (!found) {
+            // the full counting search (rmed_small_kernel)
+            float res = win[half];
+            for (int j = 0; j < width; ++j) {
+                const float v = win[j];
+                int less, leq;
+                rank_of(win, width, v, less, leq);
+                if (less <= half && half < leq) { res = v; break; }
+            }
+            m = res;
+        }
+        have = true;
+        out[ib + r] = m;
+    }
+}
+
 __device__ __forceinline__ uint32_t float_key(float v)
 {
     const uint32_t b = __float_as_uint(v);
@@ -190,9 +291,14 @@ hipError_t launch_running_median(const float* x, uint64_t n, uint32_t width, flo
                                  uint64_t out_stride, uint32_t batch, hipStream_t s)
 {
     if (!n || !batch) return hipSuccess;
-    if (width <= (uint32_t)kRmedSmallMax) {
+    if (width <= (uint32_t)kRmedSmallMax && std::getenv("RIPTIDE_AMD_RMED_COUNTING")) {
+        // A/B: one counting search per output
         hipLaunchKernelGGL(rmed_small_kernel, dim3((uint32_t)((n + kRmedTile - 1) / kRmedTile), batch),
                            dim3(kRmedTile), 0, s, x, n, (int)width, out, x_stride, out_stride);
+    } else if (width <= (uint32_t)kRmedSmallMax) {
+        const uint64_t per = (uint64_t)kRmedTile * kRmedRun;
+        hipLaunchKernelGGL(rmed_run_kernel, dim3((uint32_t)((n + per - 1) / per), batch), dim3(kRmedTile), 0, s, x, n,
+                           (int)width, out, x_stride, out_stride);
     } else {
         hipLaunchKernelGGL(rmed_large_kernel, dim3((uint32_t)n, batch), dim3(256), 0, s, x, n, (int)width,
                            out, x_stride, out_stride);
@@ -302,6 +408,59 @@ __device__ double np_interp_at(uint64_t i, const float* __restrict__ fp, uint64_
     return __dadd_rn(__dmul_rn(slope, __dsub_rn(xv, xp(j))), y0);
 }
 
+// The segment slopes of np_interp_at, computed once per segment instead of
+// once per sample: slope[j] = (fp[j + 1] - fp[j]) / (xp[j + 1] - xp[j]), the
+// same float64 operations.
+__global__ __launch_bounds__(256) void interp_slope_kernel(const float* __restrict__ fp, uint64_t n_lo, uint32_t factor,
+                                                           double* __restrict__ slope, uint64_t lo_stride)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j + 1 >= n_lo) return;
+    fp += (uint64_t)blockIdx.y * lo_stride;
+    slope += (uint64_t)blockIdx.y * lo_stride;
+    const double c = 0.5 * ((double)factor - 1.0);
+    const double x0 = (double)(j * (uint64_t)factor) + c, x1 = (double)((j + 1) * (uint64_t)factor) + c;
+    slope[j] = __ddiv_rn(__dsub_rn((double)fp[j + 1], (double)fp[j]), __dsub_rn(x1, x0));
+}
+
+// np_interp_at with 32-bit indices (series below 2^31 samples: every double
+// below is an exact small integer or half-integer), the segment index by
+// integer arithmetic (xp[j] = j * factor + c, c = (factor - 1) / 2: j =
+// floor((2i - factor + 1) / (2 factor)) for xv >= xp[0], exact; the guards of
+// np_interp_at kept) and the slope from the table: the same float64 result.
+__device__ __forceinline__ double np_interp_fast(uint32_t i, const float* __restrict__ fp,
+                                                 const double* __restrict__ slope, uint32_t n_lo, uint32_t factor)
+{
+    const double c = 0.5 * ((double)factor - 1.0);
+    const double xv = (double)i;
+    auto xp = [&](uint32_t j) { return (double)(j * factor) + c; };
+    const uint32_t last = n_lo - 1;
+    if (n_lo == 1 || xv < c) return (double)fp[0];
+    if (xv > xp(last)) return (double)fp[last];
+    uint32_t j = (2u * i + 1u - factor) / (2u * factor);
+    if (j > last) j = last;
+    while (j > 0 && xp(j) > xv) --j;
+    while (j < last && xp(j + 1) <= xv) ++j;
+    if (j == last || xp(j) == xv) return (double)fp[j];
+    return __dadd_rn(__dmul_rn(slope[j], __dsub_rn(xv, xp(j))), (double)fp[j]);
+}
+
+// out[i] = float32(x[i] - interp(i))  (time_series.py:118-122), the slopes
+// from interp_slope_kernel (factor > 1, n < 2^31)
+__global__ __launch_bounds__(256) void deredden_slope_kernel(const float* __restrict__ x, uint32_t n,
+                                                             const float* __restrict__ fp, const double* __restrict__ slope,
+                                                             uint32_t n_lo, uint32_t factor, float* __restrict__ out,
+                                                             uint64_t x_stride, uint64_t lo_stride, uint64_t out_stride)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    x += (uint64_t)blockIdx.y * x_stride;
+    fp += (uint64_t)blockIdx.y * lo_stride;
+    slope += (uint64_t)blockIdx.y * lo_stride;
+    out += (uint64_t)blockIdx.y * out_stride;
+    out[i] = (float)__dsub_rn((double)x[i], np_interp_fast(i, fp, slope, n_lo, factor));
+}
+
 // out[i] = float32(x[i] - interp(i))  (time_series.py:118-122)
 __global__ __launch_bounds__(256) void deredden_subtract_kernel(const float* __restrict__ x, uint64_t n,
                                                                 const float* __restrict__ fp, uint64_t n_lo,
@@ -319,9 +478,17 @@ __global__ __launch_bounds__(256) void deredden_subtract_kernel(const float* __r
 
 hipError_t launch_deredden_subtract(const float* x, uint64_t n, const float* rmed_lo, uint64_t n_lo,
                                     uint32_t factor, float* out, uint64_t x_stride, uint64_t lo_stride,
-                                    uint64_t out_stride, uint32_t batch, hipStream_t s)
+                                    uint64_t out_stride, uint32_t batch, hipStream_t s, double* slopes)
 {
     if (!n || !batch) return hipSuccess;
+    if (slopes && factor > 1 && n_lo > 1 && n < (1ull << 31) && !std::getenv("RIPTIDE_AMD_INTERP_PER_SAMPLE")) {
+        hipLaunchKernelGGL(interp_slope_kernel, dim3((uint32_t)((n_lo + 255) / 256), batch), dim3(256), 0, s, rmed_lo,
+                           n_lo, factor, slopes, lo_stride);
+        hipLaunchKernelGGL(deredden_slope_kernel, dim3((uint32_t)((n + 255) / 256), batch), dim3(256), 0, s, x,
+                           (uint32_t)n, rmed_lo, (const double*)slopes, (uint32_t)n_lo, factor, out, x_stride, lo_stride,
+                           out_stride);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(deredden_subtract_kernel, dim3((uint32_t)((n + 255) / 256), batch), dim3(256), 0, s,
                        x, n, rmed_lo, n_lo, factor, out, x_stride, lo_stride, out_stride);
     return hipGetLastError();

@@ -279,6 +279,7 @@ struct DevicePlan {
                 d.slot_words = h[kHdrSlotWords];
                 d.run_off = h[kHdrRunOff];
                 d.fill_chunks = h[kHdrFill];
+                d.zero_row = h[kHdrZero];
             }
             u[i] = d;
         }
@@ -784,6 +785,7 @@ void run_periodogram(const rt_plan* P, const float* d_data, size_t batch, size_t
 struct DeredGeom {
     size_t sf = 1, n_lo = 0, rmed_w = 0;
     size_t lores_floats = 0, rmed_floats = 0, partial_doubles = 0;
+    size_t slope_doubles = 0;   // np.interp segment slopes (sf > 1)
 };
 constexpr uint32_t kNormBlocks = 512;
 
@@ -801,6 +803,7 @@ DeredGeom dered_geom(size_t size, size_t ws, size_t minpts, size_t batch, bool d
             g.n_lo = size / g.sf;
             g.rmed_w = minpts;
             g.lores_floats = align_up(g.n_lo * batch, 64);
+            g.slope_doubles = align_up(g.n_lo * batch, 32);
         }
         if (!(g.rmed_w % 2)) throw std::invalid_argument("width must be an odd number");
         if (!(g.rmed_w < g.n_lo)) throw std::invalid_argument("width must be < size");
@@ -812,7 +815,7 @@ DeredGeom dered_geom(size_t size, size_t ws, size_t minpts, size_t batch, bool d
 
 size_t dered_ws_bytes(const DeredGeom& g)
 {
-    return (g.lores_floats + g.rmed_floats) * 4 + g.partial_doubles * 8 + 256;
+    return (g.lores_floats + g.rmed_floats) * 4 + (g.slope_doubles + g.partial_doubles) * 8 + 256;
 }
 
 void run_deredden_normalise(const float* d_in, size_t size, size_t batch, size_t in_stride, const DeredGeom& g,
@@ -820,7 +823,8 @@ void run_deredden_normalise(const float* d_in, size_t size, size_t batch, size_t
 {
     float* lores = (float*)ws;
     float* rmed = lores + g.lores_floats;
-    double* partials = (double*)align_up((size_t)(rmed + g.rmed_floats), 256);
+    double* slopes = (double*)align_up((size_t)(rmed + g.rmed_floats), 256);
+    double* partials = slopes + g.slope_doubles;
     const float* cur = d_in;
     size_t cur_stride = in_stride;
     if (deredden) {
@@ -834,7 +838,7 @@ void run_deredden_normalise(const float* d_in, size_t size, size_t batch, size_t
         ck(launch_running_median(rin, g.n_lo, (uint32_t)g.rmed_w, rmed, rstride, g.n_lo, (uint32_t)batch, s),
            "running_median");
         ck(launch_deredden_subtract(d_in, size, rmed, g.n_lo, (uint32_t)g.sf, d_out, in_stride, g.n_lo, out_stride,
-                                    (uint32_t)batch, s),
+                                    (uint32_t)batch, s, g.slope_doubles ? slopes : nullptr),
            "deredden_subtract");
         cur = d_out;
         cur_stride = out_stride;

@@ -87,8 +87,16 @@ constexpr int kBlobHeader = 48;
 // step's output level at [32, 44) (0: no table)
 enum : int {
     kHdrRows = 0, kHdrDesc = 12, kHdrRuns = 24, kHdrEntries = 25, kHdrBottom = 26, kHdrSlotWords = 27,
-    kHdrRunOff = 28, kHdrFill = 29, kHdrSlotOff = 32
+    kHdrRunOff = 28, kHdrFill = 29, kHdrZero = 30, kHdrSlotOff = 32
 };
+// kHdrZero: LDS float offset of a whole unit's zero row (0: none).  A 4/5-slot
+// whole unit with an even number of levels fuses every step, its deepest one
+// included, although that step's middle level holds carried size-1 nodes: a
+// carried node's missing tail operand reads a row of -0.0 (x + (-0.0) == x,
+// the reference's copy), laid after the unit's fill -- three LDS passes
+// instead of four (single, fused, fused, single).  Only the deepest step reads
+// it; a final unit's output level may cover it, so final units rewrite it
+// before every trial.
 // row slots (merge steps of units with a blob, SMAX <= 5): a wave's register
 // rows 2q, 2q + 1 hold slot q: one row, two independent rows, or a row pair
 // r, r + 1 with the same head and tail rows and roll shifts s, s + 1 (the
@@ -258,7 +266,8 @@ struct UnitDesc {
     // the unit's DMA after one scalar load instead of a dependent chain
     uint32_t nruns, entries, nb, slot_words, run_off;
     uint32_t fill_chunks;  // 16-byte chunks of the bottom-level fill
-    uint32_t pad2[2];
+    uint32_t zero_row;     // the blob's kHdrZero: LDS float offset of the unit's -0.0 row (0: none)
+    uint32_t pad2;
 };
 static_assert(sizeof(UnitDesc) == 96, "UnitDesc layout");
 

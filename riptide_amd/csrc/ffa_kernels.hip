@@ -273,6 +273,7 @@ struct UnitView {
     uint32_t blob;            // word offset of the host-built blob (kNoBlob: none)
     int nruns, entries, nb, slot_words, run_off;   // its header counts
     int fill_chunks;          // 16-byte chunks of the bottom-level fill
+    int zero_row;             // LDS float offset of the unit's -0.0 row (0: none; kHdrZero)
 };
 
 typedef const __attribute__((address_space(4))) uint32_t* const_u32_ptr;
@@ -312,6 +313,7 @@ __device__ __forceinline__ UnitView unit_view(const ConeArgs& a, int item, int t
     v.slot_words = uni((int)d.slot_words);
     v.run_off = uni((int)d.run_off);
     v.fill_chunks = uni((int)d.fill_chunks);
+    v.zero_row = uni((int)d.zero_row);
     return v;
 }
 
@@ -492,6 +494,10 @@ __device__ __forceinline__ UnitCtx unit_begin(const ConeArgs& a, uint32_t item, 
             if (SMAX == 4 && C.slots) ok = ok && words <= kLut4Off;
             // the 4/5-slot instances run row-slot steps only (merge_levels)
             if (resolved_slots(SMAX)) ok = ok && (U.levels == 0 || (C.slots && (a.flags & kConeFuse2)));
+            // the zero row of an all-fused whole unit: past its fill, inside the level buffer
+            if (U.zero_row)
+                ok = ok && resolved_slots(SMAX) && !C.tile && U.zero_row >= 4 * U.fill_chunks &&
+                     U.zero_row + 64 * SMAX <= kLdsDataFloats;
         }
         ok = ok && words >= kBlobHeader + C.entries + C.nb && C.nruns <= 64 * kConeWaves && (words & 3) == 0;
     }
@@ -1573,9 +1579,11 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
         // refuses a unit without them), so the dense per-level paths below are
         // compiled out of these, the hottest instances
         if (resolved_slots(SMAX) || (C.slots && fuse)) {
-            // row-slot steps (the host's slot tables follow this step order)
+            // row-slot steps (the host's slot tables follow this step order;
+            // a unit with a zero row fuses every step)
+            const bool all2 = C.U.zero_row != 0;
             for (int l = L - 1; l >= 0;) {
-                const bool two = l >= 1 && (tile || (node_size >> l) >= 2);
+                const bool two = l >= 1 && (tile || all2 || (node_size >> l) >= 2);
                 const int lo = two ? l - 1 : l;
                 float v[RW][SMAX];
                 const bool first = l == L - 1;
@@ -2365,6 +2373,11 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
     // DMA may still be writing), published by the barrier below
     if constexpr (SMAX == 4)
         if (C.slots && ok) build_roll_lut4(aux + kLut4Off, p, tid);
+    // the -0.0 row of an all-fused whole unit (past the fill: no trial's DMA
+    // or merge level writes it, so once per workgroup)
+    if constexpr (resolved_slots(SMAX))
+        if (ok && U.zero_row)
+            for (int j = tid; j < 64 * SMAX; j += kConeBlock) data[U.zero_row + j] = -0.0f;
     // the short-row roll table in the unused metadata area
     if constexpr (SMAX == kPack2)
         if (ok && p >= kPackSeg) build_pack_lut(aux, p, tid);
@@ -2491,6 +2504,11 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
         // final units (and merge-only units not stored from registers): the
         // next trial's fill once every wave is done with the level buffer
         if (!next_issued) fill_next();
+        // a final unit's output level (at the S/N stride) may have covered the
+        // zero row: rewritten for the next trial (its first step reads it)
+        if constexpr (resolved_slots(SMAX) && SNR)
+            if (U.zero_row)
+                for (int j = tid; j < 64 * SMAX; j += kConeBlock) data[U.zero_row + j] = -0.0f;
         ++k;
         C.U.trial = trial + 1;
 #ifdef RT_STAMPS

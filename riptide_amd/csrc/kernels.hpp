@@ -71,7 +71,7 @@ hipError_t launch_scrunch(const float* x, uint64_t n_out, uint32_t factor, float
                           uint64_t out_stride, uint32_t batch, hipStream_t s);
 hipError_t launch_deredden_subtract(const float* x, uint64_t n, const float* rmed_lo, uint64_t n_lo,
                                     uint32_t factor, float* out, uint64_t x_stride, uint64_t lo_stride,
-                                    uint64_t out_stride, uint32_t batch, hipStream_t s);
+                                    uint64_t out_stride, uint32_t batch, hipStream_t s, double* slopes = nullptr);
 hipError_t launch_interp(uint64_t n, const float* rmed_lo, uint64_t n_lo, uint32_t factor, double* out,
                          hipStream_t s);
 hipError_t launch_normalise(const float* x, uint64_t n, float* out, double* d_partials, uint32_t nblocks,

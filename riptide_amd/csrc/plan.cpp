@@ -615,6 +615,7 @@ void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, int smax, std:
     // step where no level below the output holds size-1 nodes)
     std::vector<uint32_t> slot_area;
     uint32_t slot_off[kMaxLevels + 1] = {};
+    uint32_t zero_row = 0;
     if (packed) {
         // kPack2: every lane resolves its own row, so a two-level step gets
         // its rows pre-resolved (one 8-byte read per row instead of three
@@ -659,6 +660,10 @@ void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, int smax, std:
         for (int l = 0; l <= L; ++l)
             if (fused[l]) slot_off[l] = base + rel[l];
     } else if (resolved) {
+        // whole units with an even number of levels fuse every step: the
+        // deepest step's carried (size-1) middle-level nodes read their
+        // missing operand from a -0.0 row past the fill (kHdrZero)
+        if (!tile && L >= 2 && (L % 2) == 0 && 4 * cb + 64 * (uint32_t)smax <= (uint32_t)kLdsDataFloats) zero_row = 4 * cb;
         // 4/5-slot variants: every step's row slots with their rows resolved
         // (resolved_slots): a lane reads its slot's row A (lanes 0-31) or row
         // B (32-63) as one 16-byte entry -- LDS offsets of the source rows
@@ -670,7 +675,7 @@ void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, int smax, std:
         const uint32_t base = (base0 + 3u) & ~3u;       // 16-byte aligned tables
         slot_area.assign(base - base0, 0u);
         for (int l = L - 1; l >= 0;) {
-            const bool two = l >= 1 && (tile || (it.node_size >> l) >= 2);
+            const bool two = l >= 1 && (tile || zero_row || (it.node_size >> l) >= 2);
             const int lo = two ? l - 1 : l;
             const bool first = l == L - 1;
             build_row_slots(desc + doff[lo], nrows[lo], p, slot_rw, sl);
@@ -682,9 +687,15 @@ void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, int smax, std:
                 if (two) {
                     const uint32_t dh = desc[doff[lo + 1] + (d0 & 1023u)];
                     const uint32_t dt = desc[doff[lo + 1] + ((d0 >> 10) & 1023u)];
-                    const uint32_t sh = d0 >> 20, sH = dh >> 20, sTT = ((d0 >> 20) + (dt >> 20)) % p;
-                    e[0] = off(dh & 1023u) | (off((dh >> 10) & 1023u) << 16);
-                    e[1] = off(dt & 1023u) | (off((dt >> 10) & 1023u) << 16);
+                    // a carried middle-level node: its row is the level-below
+                    // row plus the -0.0 row (zero_row; only the deepest step)
+                    const bool ch = ((dh >> 10) & 1023u) == kCarriedRow, ct = ((dt >> 10) & 1023u) == kCarriedRow;
+                    if ((ch || ct) && !(zero_row && first))
+                        throw std::runtime_error("schedule: fused step over carried nodes without a zero row");
+                    const uint32_t sh = d0 >> 20, sH = ch ? 0u : dh >> 20;
+                    const uint32_t sTT = ((d0 >> 20) + (ct ? 0u : dt >> 20)) % p;
+                    e[0] = off(dh & 1023u) | ((ch ? zero_row : off((dh >> 10) & 1023u)) << 16);
+                    e[1] = off(dt & 1023u) | ((ct ? zero_row : off((dt >> 10) & 1023u)) << 16);
                     e[2] = sH | (sh << 10) | (sTT << 20);
                 } else {
                     const uint32_t tc = (d0 >> 10) & 1023u, car = tc == kCarriedRow;
@@ -757,6 +768,7 @@ void build_tile_blob(const ConeItem& it, uint32_t p, int slot_rw, int smax, std:
     w[kHdrSlotWords] = (uint32_t)slot_area.size();
     w[kHdrRunOff] = (uint32_t)runoff;
     w[kHdrFill] = cb;
+    w[kHdrZero] = zero_row;
     if (entries) std::copy(desc_v.begin(), desc_v.begin() + entries, w + kBlobHeader);
     std::copy(loff_v.begin(), loff_v.end(), w + kBlobHeader + entries);
     std::copy(slot_area.begin(), slot_area.end(), w + kBlobHeader + entries + nb);
@@ -835,8 +847,11 @@ static void validate_blob(const ConeItem& it, uint32_t p, int smax, int rw, cons
     }
     if (resolved_slots(smax)) {
         const int Q = (rw + 1) / 2;
+        const uint32_t zero_row = w[kHdrZero];
+        if (zero_row && (tile || (L % 2) || zero_row < 4 * fill || zero_row + 64 * (uint32_t)smax > (uint32_t)kLdsDataFloats))
+            throw std::runtime_error("schedule: bad zero row");
         for (int l = (int)L - 1; l >= 0;) {
-            const bool two = l >= 1 && (tile || (it.node_size >> l) >= 2);
+            const bool two = l >= 1 && (tile || zero_row || (it.node_size >> l) >= 2);
             const int lo = two ? l - 1 : l;
             const uint32_t n = w[kHdrRows + lo], so = w[kHdrSlotOff + lo];
             if ((so & 3u) || so < (uint32_t)kBlobHeader + nb || so + 4 > runoff)

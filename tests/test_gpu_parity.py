@@ -264,6 +264,28 @@ def test_batch_matches_single(rt):
         assert np.array_equal(dn[b].cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("tpw", ["1", "2", "3", "16"])
+@pytest.mark.parametrize("ci", [0, 1, 3, 4])
+def test_trials_per_workgroup(rt, monkeypatch, tpw, ci):
+    """Workgroups running several trials of an item (RIPTIDE_AMD_TRIALS_PER_WG,
+    ConeArgs::trials_per_wg; 16 by default): a batch of 5 distinct trials --
+    T = 2 and 3 leave a partial last group -- bit-identical to each trial run
+    alone, for the 4/5-slot rows (cfg2 / cfg1 search parameters) and the
+    short rows (cfg4) and the 16-slot rows (800-1200 bins)."""
+    import torch
+    from riptide_amd import engine
+    case = inputs.PGRAM_CASES[ci]
+    monkeypatch.setenv("RIPTIDE_AMD_TRIALS_PER_WG", tpw)
+    plan = engine.PeriodogramPlan.for_search(case["n"], case["tsamp"], case["pmin"], case["pmax"],
+                                             case["bmin"], case["bmax"], ducy_max=case["ducy_max"])
+    xs = np.stack([inputs.with_signal(case["n"], case["tsamp"], s, case["period"], 12.0) for s in range(5)])
+    d = torch.from_numpy(xs).cuda()
+    batch = plan.run(d, check=True).cpu().numpy()
+    for b in range(5):
+        single = plan.run(d[b:b + 1].contiguous(), check=True).cpu().numpy()[0]
+        assert np.array_equal(batch[b], single), f"trial {b} differs in a batch at {tpw} trials per workgroup"
+
+
 def test_ladder_passes_pipeline_matches_run(rt):
     """rt_periodogram_ladder_device + rt_periodogram_passes_device (the two
     halves a pipelined caller runs on two streams, bench.py --overlap 1) give

@@ -14,6 +14,7 @@
 #   bash tools/gpu_run.sh TAG stamps CFG             per-phase stamps (libriptide_amd_stamps.so)
 #   bash tools/gpu_run.sh TAG trace LIB...           per-launch cone durations of the cfg2 bench per library
 #   bash tools/gpu_run.sh TAG parity LIB...          GPU parity tests (test_gpu_parity.py) per library
+#   bash tools/gpu_run.sh TAG pmclib CFG LIB...      SQ counter groups of the cone kernel per library
 #   bash tools/gpu_run.sh TAG pmcflags CFG FLAGS...  instruction counters per RIPTIDE_AMD_CONE_FLAGS value
 #                                                    (diagnostic bits: phase attribution of VALU / SALU / LDS)
 #   bash tools/gpu_run.sh TAG round                  round-end pass: pmc (cfg2, cfg3, cfg4), tests, smoke,
@@ -165,6 +166,30 @@ PY
   done
 }
 
+do_pmclib() {   # CFG LIB...: the SQ counter groups of the cone kernel per library (tools/ab_flags.py, flags 7)
+  local cfg=$1; shift
+  for lib in "$@"; do
+    local n=$(basename "$lib" .so) i=0
+    for grp in "${PMC_GROUPS[@]:0:2}"; do
+      i=$((i+1))
+      local d="$O/pmclib_${cfg}_${n}_p$i"
+      (cd /tmp && export TMPDIR=/tmp && RIPTIDE_AMD_LIB=$R/$lib timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace -f csv \
+         -d "$d" -o run -- python3 "$R/tools/ab_flags.py" 7 "$cfg" > "$d.log" 2>&1) || fail "pmclib $n $i" "$d.log"
+    done
+    python3 - "$O" "pmclib_${cfg}_${n}" <<'PY'
+import csv, glob, sys
+from collections import defaultdict
+S = defaultdict(float); t = 0.0
+for fn in glob.glob(sys.argv[1] + "/" + sys.argv[2] + "_p*/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(fn)):
+        if "cone_kernel" in r.get("Kernel_Name", ""):
+            S[r["Counter_Name"]] += float(r["Counter_Value"])
+tr = 64.0
+print(sys.argv[2], "per trial:", {k: "%.4g" % (v / tr) for k, v in sorted(S.items())})
+PY
+  done
+}
+
 case "$CMD" in
   tests) do_tests ;;
   bench) do_bench bench "$@" ;;
@@ -177,6 +202,7 @@ case "$CMD" in
   trace) do_trace "$@" ;;
   parity) do_parity "$@" ;;
   pmcflags) do_pmcflags "$@" ;;
+  pmclib) do_pmclib "$@" ;;
   round)
     do_pmc cfg2
     do_pmc cfg3
