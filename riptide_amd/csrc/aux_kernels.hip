@@ -452,6 +452,33 @@ __global__ __launch_bounds__(256) void deredden_slope_kernel(const float* __rest
                                                              uint32_t n_lo, uint32_t factor, float* __restrict__ out,
                                                              uint64_t x_stride, uint64_t lo_stride, uint64_t out_stride)
 {
+    // four consecutive samples per thread: 16-byte loads and stores where the
+    // rows are 16-byte aligned (the launch checks the strides and bases)
+    const uint32_t i0 = 4u * (blockIdx.x * 256u + threadIdx.x);
+    if (i0 >= n) return;
+    x += (uint64_t)blockIdx.y * x_stride;
+    fp += (uint64_t)blockIdx.y * lo_stride;
+    slope += (uint64_t)blockIdx.y * lo_stride;
+    out += (uint64_t)blockIdx.y * out_stride;
+    if (i0 + 4 <= n) {
+        const float4 v = *reinterpret_cast<const float4*>(x + i0);
+        float4 r;
+        r.x = (float)__dsub_rn((double)v.x, np_interp_fast(i0, fp, slope, n_lo, factor));
+        r.y = (float)__dsub_rn((double)v.y, np_interp_fast(i0 + 1, fp, slope, n_lo, factor));
+        r.z = (float)__dsub_rn((double)v.z, np_interp_fast(i0 + 2, fp, slope, n_lo, factor));
+        r.w = (float)__dsub_rn((double)v.w, np_interp_fast(i0 + 3, fp, slope, n_lo, factor));
+        *reinterpret_cast<float4*>(out + i0) = r;
+    } else {
+        for (uint32_t i = i0; i < n; ++i) out[i] = (float)__dsub_rn((double)x[i], np_interp_fast(i, fp, slope, n_lo, factor));
+    }
+}
+
+// the one-sample-per-thread form (rows not 16-byte aligned)
+__global__ __launch_bounds__(256) void deredden_slope1_kernel(const float* __restrict__ x, uint32_t n,
+                                                              const float* __restrict__ fp, const double* __restrict__ slope,
+                                                              uint32_t n_lo, uint32_t factor, float* __restrict__ out,
+                                                              uint64_t x_stride, uint64_t lo_stride, uint64_t out_stride)
+{
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= n) return;
     x += (uint64_t)blockIdx.y * x_stride;
@@ -484,9 +511,16 @@ hipError_t launch_deredden_subtract(const float* x, uint64_t n, const float* rme
     if (slopes && factor > 1 && n_lo > 1 && n < (1ull << 31) && !std::getenv("RIPTIDE_AMD_INTERP_PER_SAMPLE")) {
         hipLaunchKernelGGL(interp_slope_kernel, dim3((uint32_t)((n_lo + 255) / 256), batch), dim3(256), 0, s, rmed_lo,
                            n_lo, factor, slopes, lo_stride);
-        hipLaunchKernelGGL(deredden_slope_kernel, dim3((uint32_t)((n + 255) / 256), batch), dim3(256), 0, s, x,
-                           (uint32_t)n, rmed_lo, (const double*)slopes, (uint32_t)n_lo, factor, out, x_stride, lo_stride,
-                           out_stride);
+        const bool vec = ((uintptr_t)x % 16) == 0 && ((uintptr_t)out % 16) == 0 && x_stride % 4 == 0 &&
+                         out_stride % 4 == 0;
+        if (vec)
+            hipLaunchKernelGGL(deredden_slope_kernel, dim3((uint32_t)((n + 1023) / 1024), batch), dim3(256), 0, s, x,
+                               (uint32_t)n, rmed_lo, (const double*)slopes, (uint32_t)n_lo, factor, out, x_stride,
+                               lo_stride, out_stride);
+        else
+            hipLaunchKernelGGL(deredden_slope1_kernel, dim3((uint32_t)((n + 255) / 256), batch), dim3(256), 0, s, x,
+                               (uint32_t)n, rmed_lo, (const double*)slopes, (uint32_t)n_lo, factor, out, x_stride,
+                               lo_stride, out_stride);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(deredden_subtract_kernel, dim3((uint32_t)((n + 255) / 256), batch), dim3(256), 0, s,
@@ -561,6 +595,30 @@ __global__ __launch_bounds__(kNormBlock) void norm_finalize_kernel(const double*
     if (threadIdx.x == 0) stats[2 * blockIdx.x + mode] = t / (double)n;
 }
 
+// four samples per thread (16-byte aligned rows; norm_apply_kernel otherwise)
+__global__ __launch_bounds__(256) void norm_apply4_kernel(const float* __restrict__ x, uint64_t n,
+                                                          const double* __restrict__ stats, float* __restrict__ out,
+                                                          uint64_t x_stride, uint64_t out_stride)
+{
+    const uint64_t i0 = 4 * ((uint64_t)blockIdx.x * 256 + threadIdx.x);
+    if (i0 >= n) return;
+    const double mean = stats[2 * blockIdx.y], var = stats[2 * blockIdx.y + 1];
+    const double norm = sqrt(var);
+    x += (uint64_t)blockIdx.y * x_stride;
+    out += (uint64_t)blockIdx.y * out_stride;
+    if (i0 + 4 <= n) {
+        const float4 v = *reinterpret_cast<const float4*>(x + i0);
+        float4 r;
+        r.x = (float)__ddiv_rn(__dsub_rn((double)v.x, mean), norm);
+        r.y = (float)__ddiv_rn(__dsub_rn((double)v.y, mean), norm);
+        r.z = (float)__ddiv_rn(__dsub_rn((double)v.z, mean), norm);
+        r.w = (float)__ddiv_rn(__dsub_rn((double)v.w, mean), norm);
+        *reinterpret_cast<float4*>(out + i0) = r;
+    } else {
+        for (uint64_t i = i0; i < n; ++i) out[i] = (float)__ddiv_rn(__dsub_rn((double)x[i], mean), norm);
+    }
+}
+
 __global__ __launch_bounds__(256) void norm_apply_kernel(const float* __restrict__ x, uint64_t n,
                                                          const double* __restrict__ stats, float* __restrict__ out,
                                                          uint64_t x_stride, uint64_t out_stride)
@@ -585,8 +643,12 @@ hipError_t launch_normalise(const float* x, uint64_t n, float* out, double* d_pa
         hipLaunchKernelGGL(norm_finalize_kernel, dim3(batch), dim3(kNormBlock), 0, s, d_partials, nblocks, n,
                            stats, mode);
     }
-    hipLaunchKernelGGL(norm_apply_kernel, dim3((uint32_t)((n + 255) / 256), batch), dim3(256), 0, s, x, n, stats,
-                       out, x_stride, out_stride);
+    if (((uintptr_t)x % 16) == 0 && ((uintptr_t)out % 16) == 0 && x_stride % 4 == 0 && out_stride % 4 == 0)
+        hipLaunchKernelGGL(norm_apply4_kernel, dim3((uint32_t)((n + 1023) / 1024), batch), dim3(256), 0, s, x, n,
+                           stats, out, x_stride, out_stride);
+    else
+        hipLaunchKernelGGL(norm_apply_kernel, dim3((uint32_t)((n + 255) / 256), batch), dim3(256), 0, s, x, n, stats,
+                           out, x_stride, out_stride);
     return hipGetLastError();
 }
 

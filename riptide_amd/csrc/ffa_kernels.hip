@@ -1106,11 +1106,66 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
 // Slot-step write-back into the dense LDS rows at base / store to global
 // memory (a non-final pass's output level): register rows 2q, 2q + 1 to the
 // slot's rows A and B (row stride q: p, or a final pass's S/N stride).
+#ifndef RT_NO_ADDTID_WRITES
+// A row's full 64-bin slots (all but the last) by ds_write_addtid_b32: the
+// address is M0 + offset + 4 lane (no address VGPR), 2 LDS cycles per wave
+// instruction instead of ds_write_b32's 4.  M0 holds 16 bits: rows past
+// 64 KiB - 1 KiB take M0 = a - 32 KiB and offsets from 32 KiB.  Same-box
+// A/B, cone ms per trial (profiles/r05q_ab_*.log): cfg2 6.56-6.58 vs
+// 6.59-6.62, cfg3 1.658-1.693 vs 1.670-1.697 (RT_NO_ADDTID_WRITES: the
+// ds_write_b32 form).
+template <int SMAX>
+__device__ __forceinline__ void write_row_addtid(uint32_t a, const float (&x)[SMAX])
+{
+    static_assert(SMAX == 4 || SMAX == 5, "4/5-slot rows");
+    if (a <= 0xFFFFu - 256u * (SMAX - 2)) {
+        if constexpr (SMAX == 4)
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tds_write_addtid_b32 %1\n\tds_write_addtid_b32 %2 offset:256\n\t"
+                         "ds_write_addtid_b32 %3 offset:512"
+                         :: "s"(a), "v"(x[0]), "v"(x[1]), "v"(x[2]) : "memory", "m0");
+        else
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tds_write_addtid_b32 %1\n\tds_write_addtid_b32 %2 offset:256\n\t"
+                         "ds_write_addtid_b32 %3 offset:512\n\tds_write_addtid_b32 %4 offset:768"
+                         :: "s"(a), "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]) : "memory", "m0");
+    } else {
+        const uint32_t b = a - 32768u;
+        if constexpr (SMAX == 4)
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tds_write_addtid_b32 %1 offset:32768\n\t"
+                         "ds_write_addtid_b32 %2 offset:33024\n\tds_write_addtid_b32 %3 offset:33280"
+                         :: "s"(b), "v"(x[0]), "v"(x[1]), "v"(x[2]) : "memory", "m0");
+        else
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tds_write_addtid_b32 %1 offset:32768\n\t"
+                         "ds_write_addtid_b32 %2 offset:33024\n\tds_write_addtid_b32 %3 offset:33280\n\t"
+                         "ds_write_addtid_b32 %4 offset:33536"
+                         :: "s"(b), "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]) : "memory", "m0");
+    }
+}
+#endif
+
 template <int SMAX, int RW>
 __device__ __forceinline__ void write_rows_slots(float* base, float* dummy, const float (&v)[RW][SMAX], int p,
                                                  int lane, uint32_t sw, int nq, int q)
 {
     const bool tail_ok = lane + 64 * (SMAX - 1) < p;
+#ifndef RT_NO_ADDTID_WRITES
+    if constexpr (resolved_slots(SMAX)) {
+        typedef __attribute__((address_space(3))) float* lds_fptr;
+        const uint32_t b0 = (uint32_t)(uintptr_t)(lds_fptr)base;
+#pragma unroll
+        for (int i = 0; i < RW; ++i) {
+            if (i / 2 < nq) {
+                const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)sw, i / 2);
+                if (i % 2 == 0 || (w >> 20) != kSlotOne) {
+                    const int row = (int)((i % 2 == 0 ? w : w >> 10) & 1023u);
+                    write_row_addtid<SMAX>(b0 + 4u * (uint32_t)(row * q), v[i]);
+                    float* orow = base + row * q + lane;
+                    *(tail_ok ? orow + 64 * (SMAX - 1) : dummy) = v[i][SMAX - 1];
+                }
+            }
+        }
+        return;
+    }
+#endif
 #pragma unroll
     for (int i = 0; i < RW; ++i) {
         if (i / 2 < nq) {
