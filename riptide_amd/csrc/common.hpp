@@ -74,6 +74,25 @@ RT_HD constexpr int snr_group(int p)
     while (G < 64 && ((((p + G - 1) / G) | 1) > kSnrMaxChunk)) G <<= 1;
     return G;
 }
+// Segmented S/N (ffa_kernels.hip snr_segments): a final level of <= 64 rows
+// of 240-264 bins, widths <= 9, one row per lane, each of the 8 waves a
+// segment of kSnrSegCols columns.  Row r lies in an LDS slot of
+// kSnrSegStride floats (odd: 64 rows on distinct banks) at offset
+// 8 kSnrSegCols - p, so the first segment starts at the slot start; the
+// segment sums are exchanged through kSnrSegExch floats at the end of the
+// level buffer (past kLdsDataFloats: the fill slack is dead by then).
+constexpr int kSnrSegCols = 33;
+constexpr int kSnrSegWmax = 9;
+constexpr int kSnrSegRows = 64;
+constexpr int kSnrSegStride = 8 * kSnrSegCols + 1;
+constexpr int kSnrSegExch = 2 * 64 * 8;
+static_assert(kSnrSegRows * kSnrSegStride <= kLdsDataFloats, "segmented S/N rows");
+static_assert(kSnrSegRows * kSnrSegStride + kSnrSegExch <= kLdsBufFloats, "segmented S/N exchange area");
+RT_HD inline bool snr_seg_ok(int p, int wmax, int rows)
+{
+    return p >= 8 * kSnrSegCols - 24 && p <= 8 * kSnrSegCols && wmax >= 1 && wmax <= kSnrSegWmax && rows >= 1 &&
+           rows <= kSnrSegRows;
+}
 constexpr int kStageRegs = 45 * 8 / kConeWaves;   // merge: staged values per lane (rows x slots)
 constexpr int kMaxSlots = 45;               // merge: 64-bin slots per row (p <= 2880)
 constexpr int kMaxRowsPerWave = 24;         // merge: staged rows per wave
@@ -228,6 +247,7 @@ enum : uint32_t {
     kConeStoreFromRegs = 1u,   // non-final passes store the output level straight from registers
     kConeFuse2 = 2u,           // two merge levels per LDS round trip where no level holds size-1 nodes
     kConeSnrStride = 4u,       // final passes keep their output rows at a bank-friendly stride for the S/N
+    kConeSnrSeg = 8u,          // final passes of 240-264-bin rows with widths <= 9: the segmented S/N (snr_segments)
     kConeDiagNoSnr = 1u << 30, // diagnostics only (wrong results): skip the S/N epilogue
     kConeDiagNoMerge = 1u << 29, // diagnostics only (wrong results): skip the merge levels
     kConeDiagNoWrite = 1u << 28, // diagnostics only (wrong results): skip the level write-back
@@ -235,7 +255,7 @@ enum : uint32_t {
     kConeDiagNoLand = 1u << 26,  // diagnostics only (wrong results): fill loads issued but not landed in LDS
     kConeDiagNoDesc = 1u << 25,  // diagnostics only (wrong results): no descriptor table
     kConeDiagNoFill = 1u << 23,  // diagnostics only (wrong results): metadata DMA only, no bottom-level fill
-    kConeDefaultFeatures = 7u   // kConeSnrStride: final-pass rows at a stride with room for the S/N wrap extension
+    kConeDefaultFeatures = 15u  // every feature bit above
 };
 enum : uint8_t { kSelLeaves = 0, kSelPing = 1, kSelPong = 2, kSelSnr = 3 };
 

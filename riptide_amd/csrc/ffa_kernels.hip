@@ -1536,11 +1536,12 @@ __device__ __forceinline__ void put_tasks(float* base, int q, const float (&v)[k
 // the staging registers straight to global memory instead of back into LDS.
 // pre_store(): called by every wave after the last merge step's LDS reads
 // and before its output level is stored from registers (st): the level
-// buffer is then free for the next trial's fill.
+// buffer is then free for the next trial's fill.  A final pass's output
+// level (row-slot steps) starts oshift floats past base.
 template <int SMAX, int RW, class PreStore>
 __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int p, int L, int tid, bool st,
                                              __amdgpu_buffer_rsrc_t rs, uint32_t st_o0, uint32_t flags, float* dummy,
-                                             int qout, PreStore&& pre_store)
+                                             int qout, int oshift, PreStore&& pre_store)
 {
     const int lane = tid & 63, wave = tid >> 6;
     const bool tile = C.tile;
@@ -1657,7 +1658,8 @@ __device__ __forceinline__ void merge_levels(const UnitCtx& C, float* base, int 
                 if (!(flags & kConeDiagNoBarrier)) lds_barrier();
                 // the output level of a final pass at row stride qout (the S/N's)
                 if (!(flags & kConeDiagNoWrite))
-                    write_rows_slots<SMAX, RW>(base, dummy, v, p, lane, sw, nq, lo == 0 ? qout : p);
+                    write_rows_slots<SMAX, RW>(lo == 0 ? base + oshift : base, dummy, v, p, lane, sw, nq,
+                                               lo == 0 ? qout : p);
                 if (!(flags & kConeDiagNoBarrier)) lds_barrier();
             }
             return;
@@ -2194,6 +2196,197 @@ __device__ __forceinline__ void snr_rows(const ConeArgs& a, const UnitView& U, f
     }
 }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// diff_max (kernels.hpp:50-60) of width W over the S = 2 K + 1 window starts
+// of a segment, c[0 .. S + W) in K + 5 register pairs P (P[k] = c[2k],
+// c[2k + 1]) and, for odd W, the shifted pairs H[k] = c[2k + 1], c[2k + 2]:
+// max_i c[i + W] - c[i], two differences per v_pk_add_f32 (negated second
+// operand: x + (-y) == x - y, signed zeros included) and one v_max3_f32.
+template <int K, int W>
+__device__ __forceinline__ float seg_window_max(const f2v (&P)[K + 5], const f2v (&H)[K + 4])
+{
+    float dm = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const f2v hi = (W & 1) ? H[k + (W - 1) / 2] : P[k + W / 2];
+        f2v d;
+        asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(d) : "v"(hi), "v"(P[k]));
+        asm("v_max3_f32 %0, %0, %1, %2" : "+v"(dm) : "v"(d.x), "v"(d.y));
+    }
+    // the last start, 2K
+    constexpr int e = 2 * K + W;
+    const float ce = (e & 1) ? P[e / 2].y : P[e / 2].x;
+    float t;
+    asm("v_sub_f32 %1, %2, %3\n\tv_max_f32 %0, %0, %1" : "+v"(dm), "=&v"(t) : "v"(ce), "v"(P[K].x));
+    return dm;
+}
+
+// Segmented boxcar S/N (snr.hpp:37-65, kernels.hpp:50-101) of a final level
+// of 240-264-bin rows, row r at slot + r * kSnrSegStride + r0 (r0 = 8 S - p
+// <= 24 columns of slack in front of the row): lane = row, wave w = slot
+// columns [w S, w S + S).  The slack columns count as +0.0 samples and +inf
+// prefix values (selects in wave 0 only), so they add nothing to the sums and
+// never start a window.  Per block of 64 rows:
+//   A. the segment's samples into registers; their fp64 sum to the exchange
+//      area (kSnrSegExch floats at the end of the level buffer);
+//   B. the segment's offset (the sums of the segments before it, in order)
+//      and the row total; the segment's fp64 running sum, cast per column to
+//      float (circular_prefix_sum, kernels.hpp:62-80); its first 9 prefix
+//      values written back in place (wave 0: all S -- the wrap reads columns
+//      0 .. 8);
+//   C. the next segment's first 9 prefix values (the last segment: the wrap
+//      c[p + e] = c[e] + sum, kernels.hpp:88-97), then every width's window
+//      maximum over the segment's starts, written over the row's slot head;
+//   D. width iw on wave iw (mod 8): the 8 segment maxima, the S/N formula,
+//      one store per row.
+// Each lane works on its own row throughout: no cross-lane shuffles or
+// scans, 4 workgroup barriers per 64 rows.
+template <int SMAX>
+__device__ __forceinline__ void snr_segments(const ConeArgs& a, const UnitView& U, float* slot, const int* wl,
+                                             int nrows, int tid, const float* whb)
+{
+    constexpr int S = kSnrSegCols;
+    constexpr int E = kSnrSegWmax;
+    constexpr int K = S / 2;
+    constexpr int q = kSnrSegStride;
+    static_assert(S == 2 * K + 1 && 2 * (K + 5) >= S + E && 8 * S - 24 > 0, "segment shape");
+    // an opaque thread index (as snr_epilogue)
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63;
+    const int wave = uni(tid >> 6);
+    const int p = U.p;
+    const int nev = (int)min((int64_t)nrows, (int64_t)U.rows_eval - (int64_t)U.s0);
+    if (nev <= 0) return;
+    const uint32_t nw = a.num_widths;
+    const int r0 = 8 * S - p;                 // slack columns in front of the row (0 .. 24)
+    // r0 in a VGPR: the slack selects of wave 0 as v_cmp + v_cndmask (uniform
+    // masks per column were hoisted into SGPR pairs that spill)
+    int r0v = r0;
+    asm volatile("" : "+v"(r0v));
+    uint32_t wmask = 0;
+    for (uint32_t iw = 0; iw < nw; ++iw) wmask |= 1u << uni(wl[iw]);
+    double* const exch = reinterpret_cast<double*>(slot + kLdsBufFloats - kSnrSegExch);
+    float* const snr = a.snr + (uint64_t)U.trial * a.snr_stride + (U.snr_row + (uint64_t)U.s0) * (uint64_t)nw;
+    const __amdgpu_buffer_rsrc_t srs = buffer_rsrc(snr, (uint32_t)nev * nw * 4u);
+    for (int rb = 0; rb < nev; rb += 64) {
+        const int r = rb + lane;
+        const bool act = r < nev;
+        // rows past nev compute (and write) the values of row nev - 1 again
+        float* const row = slot + min(r, nev - 1) * q;
+        float* const seg = row + wave * S;
+        float c[S];
+        // A: samples and the segment sum
+#pragma unroll
+        for (int g = 0; g < S; ++g) c[g] = lds_ld((lds_cptr)(seg + g));
+        if (wave == 0) {
+            asm volatile("" : "+v"(r0v));     // per block: the compares stay in place
+#pragma unroll
+            for (int g = 0; g < 24; ++g) c[g] = g < r0v ? 0.0f : c[g];
+        }
+        // (the first addition of 0.0 dropped: a -0.0 sum is made +0.0 by
+        // the offsets' and the total's +0.0 starts)
+        double part = (double)c[0];
+#pragma unroll
+        for (int g = 1; g < S; ++g) part = part + (double)c[g];
+        exch[wave * 64 + lane] = part;
+        lds_barrier();
+        // B: offset, total, prefix values
+        double off = 0.0, tot = 0.0;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+            const double pv = exch[w * 64 + lane];
+            if (w < wave) off = off + pv;
+            tot = tot + pv;
+        }
+        const float sumx = (float)tot;
+        double acc = off;
+#pragma unroll
+        for (int g = 0; g < S; ++g) {
+            acc = acc + (double)c[g];
+            c[g] = (float)acc;
+        }
+        if (wave == 0) {
+#pragma unroll
+            for (int g = 0; g < S; ++g) seg[g] = c[g];
+        } else {
+#pragma unroll
+            for (int g = 0; g < E; ++g) seg[g] = c[g];
+        }
+        lds_barrier();
+        // C: the next segment's first prefix values, the window maxima
+        f2v P[K + 5], H[K + 4];
+#pragma unroll
+        for (int k = 0; k <= K; ++k) P[k] = f2v{c[2 * k], 2 * k + 1 < S ? c[2 * k + 1] : 0.0f};
+        float n[E];
+        if (wave < 7) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) n[e] = lds_ld((lds_cptr)(seg + S + e));
+        } else {
+            const lds_cptr w0 = (lds_cptr)(row + r0);
+#pragma unroll
+            for (int e = 0; e < E; ++e) n[e] = __fadd_rn(lds_ld(w0 + e), sumx);
+        }
+        // c[S + e] = n[e]: P[K].y, then pairs K + 1 ..
+        P[K].y = n[0];
+#pragma unroll
+        for (int k = K + 1; k < K + 5; ++k) P[k] = f2v{n[2 * (k - K) - 1], n[2 * (k - K)]};
+        if (wave == 0) {
+            asm volatile("" : "+v"(r0v));
+#pragma unroll
+            for (int g = 0; g < 24; ++g) {
+                if (g & 1) P[g / 2].y = g < r0v ? INFINITY : P[g / 2].y;
+                else P[g / 2].x = g < r0v ? INFINITY : P[g / 2].x;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K + 4; ++k) H[k] = f2v{P[k].y, P[k + 1].x};
+        float m[E + 1];
+#pragma unroll
+        for (int w = 0; w <= E; ++w) m[w] = -INFINITY;
+        constexpr uint32_t kStdMask = (1u << 1) | (1u << 2) | (1u << 3) | (1u << 4) | (1u << 6) | (1u << 9);
+        if (wmask == kStdMask) {
+            // the standard ladder 1, 2, 3, 4, 6, 9 in one block: six
+            // independent max chains for the scheduler to interleave
+            m[1] = seg_window_max<K, 1>(P, H);
+            m[2] = seg_window_max<K, 2>(P, H);
+            m[3] = seg_window_max<K, 3>(P, H);
+            m[4] = seg_window_max<K, 4>(P, H);
+            m[6] = seg_window_max<K, 6>(P, H);
+            m[9] = seg_window_max<K, 9>(P, H);
+        } else {
+            if (wmask & (1u << 1)) m[1] = seg_window_max<K, 1>(P, H);
+            if (wmask & (1u << 2)) m[2] = seg_window_max<K, 2>(P, H);
+            if (wmask & (1u << 3)) m[3] = seg_window_max<K, 3>(P, H);
+            if (wmask & (1u << 4)) m[4] = seg_window_max<K, 4>(P, H);
+            if (wmask & (1u << 5)) m[5] = seg_window_max<K, 5>(P, H);
+            if (wmask & (1u << 6)) m[6] = seg_window_max<K, 6>(P, H);
+            if (wmask & (1u << 7)) m[7] = seg_window_max<K, 7>(P, H);
+            if (wmask & (1u << 8)) m[8] = seg_window_max<K, 8>(P, H);
+            if (wmask & (1u << 9)) m[9] = seg_window_max<K, 9>(P, H);
+        }
+        lds_barrier();                        // every wave is past its reads of the rows
+#pragma unroll
+        for (int w = 1; w <= E; ++w)
+            if (wmask & (1u << w)) row[E * wave + w - 1] = m[w];
+        lds_barrier();
+        // D: width iw on wave iw (mod 8)
+        for (int iw = wave; iw < (int)nw; iw += 8) {
+            const int w = uni(wl[iw]);
+            const lds_cptr mx = (lds_cptr)(row + w - 1);
+            float dm = lds_ld(mx);
+#pragma unroll
+            for (int k = 1; k < 8; ++k) dm = fmaxf(dm, lds_ld(mx + E * k));
+            const float hpb = whb[2 * iw], b = whb[2 * iw + 1];
+            const float v = (hpb * dm - b * sumx) / U.stdnoise;
+            const uint32_t o = act ? ((uint32_t)r * nw + (uint32_t)iw) * 4u : 0x80000000u;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srs, (int)o, 0, kSnrCpol);
+        }
+        // the next block's phase-A exchange writes come after this block's
+        // phase-B reads (two barriers between); its rows are other rows
+    }
+}
+
 // Phase-bin range [lo, hi] a cone kernel variant runs, and the S/N lane-group
 // size G of a row of p bins: the epilogue instantiates only the row shapes its
 // variant can meet (smaller kernels; the rest is compiled out).
@@ -2457,6 +2650,10 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
     // chunk strides) then read and write on distinct banks (at stride p they
     // collided on up to 10 of 32 banks)
     int qout = p;
+    // the segmented S/N (snr_segments): rows of 240-264 bins, widths <= 9,
+    // <= 64 rows in slots of kSnrSegStride floats (feature bit kConeSnrSeg)
+    const bool seg_snr = SNR && resolved_slots(SMAX) && (a.flags & kConeSnrSeg) && L > 0 && C.slots &&
+                         snr_seg_ok(p, wl[kMaxWidths], n0);
     // short rows keep their blob's LDS part at the end of the level buffer,
     // which a final pass's output level (at the S/N stride) and its S/N's
     // dummy words may overwrite: every trial's fill then re-DMAs it
@@ -2480,7 +2677,9 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
         // p + kSnrWin (the extension only)
         const int qa = p + kSnrMaxChunk + ((16 - ((p + kSnrMaxChunk) & 31)) & 31);
         const int qb = p + kSnrWin + ((16 - ((p + kSnrWin) & 31)) & 31);
-        if (!st && L > 0 && C.slots && (a.flags & kConeFuse2) && (a.flags & kConeSnrStride)) {
+        if (seg_snr) {
+            qout = kSnrSegStride;
+        } else if (!st && L > 0 && C.slots && (a.flags & kConeFuse2) && (a.flags & kConeSnrStride)) {
             qout = n0 * qa <= kLdsDataFloats ? qa : (n0 * qb <= kLdsDataFloats ? qb : p);
             // widths past the register window: a stride with room for their
             // plain-LDS windows (snr_wide_stride), = 16 (mod 32) where that
@@ -2513,7 +2712,7 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
         };
         if (L > 0 && !(a.flags & kConeDiagNoMerge))
             merge_levels<SMAX, RW>(C, buf, p, L, tid, st_regs, rs, o0, a.flags, buf + kLdsBufFloats + 4 + (tid & 63),
-                                   qout, fill_next);
+                                   qout, seg_snr ? 8 * kSnrSegCols - p : 0, fill_next);
         RT_MARK(3);
         // the output level: dense rows from the buffer start, or (no merge
         // level) the single bottom row where the DMA left it
@@ -2527,11 +2726,16 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
                                                               (int)(o0 + (uint32_t)(r * p + j) * 4u), 0, kStoreCpol);
             }
         } else if constexpr (SNR) {
+            if (seg_snr) {
+                if constexpr (resolved_slots(SMAX))
+                    if (!(a.flags & kConeDiagNoSnr)) snr_segments<SMAX>(a, C.U, buf, wl, n0, tid, whb);
+            } else {
 #ifdef RT_STAMPS
-            if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(a, C.U, obase, qout, wl, n0, tid, whb, tl);
+                if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(a, C.U, obase, qout, wl, n0, tid, whb, tl);
 #else
-            if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(a, C.U, obase, qout, wl, n0, tid, whb, nullptr);
+                if (!(a.flags & kConeDiagNoSnr)) snr_epilogue<SMAX, WIDE>(a, C.U, obase, qout, wl, n0, tid, whb, nullptr);
 #endif
+            }
         }
 #ifdef RT_STAMPS
         lds_barrier();

@@ -298,8 +298,21 @@ static bool wide_snr(const FfaXform& X, int smax, bool snr_epilogue, uint32_t ma
     return true;
 }
 
+// Final tiles of the segmented S/N (ffa_kernels.hip snr_segments): one block
+// of kSnrSegRows rows; off with the kernel's feature bit
+// (RIPTIDE_AMD_CONE_FLAGS without kConeSnrSeg, A/B).
+static bool seg_snr(const FfaXform& X, int smax, bool snr_epilogue, uint32_t max_width)
+{
+    if (!snr_epilogue || (smax != 4 && smax != 5)) return false;
+    if (!snr_seg_ok((int)X.p, (int)max_width, 1)) return false;
+    if (const char* e = std::getenv("RIPTIDE_AMD_CONE_FLAGS"))
+        if (!(std::strtoul(e, nullptr, 0) & kConeSnrSeg)) return false;
+    return true;
+}
+
 static uint32_t final_tile_cap(const FfaXform& X, int smax, bool snr_epilogue, uint32_t max_width)
 {
+    if (seg_snr(X, smax, snr_epilogue, max_width)) return kSnrSegRows;
     if (!wide_snr(X, smax, snr_epilogue, max_width)) return 0;
     const int q = snr_wide_stride((int)X.p, (int)max_width);
     const int k = kLdsDataFloats / q;

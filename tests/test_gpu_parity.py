@@ -347,6 +347,40 @@ def test_wide_snr_matches_window_path(monkeypatch, ducy_max, widths):
     assert np.array_equal(out["1"][1], single)
 
 
+@pytest.mark.parametrize("widths, bins", [(None, (240, 260)), ([9, 3, 1], (240, 265)), ([1, 5, 7, 8], (240, 265)),
+                                          ([2], (250, 265))])
+def test_segmented_snr_matches_window_path(oracle, monkeypatch, widths, bins):
+    """Final units of 240-264-bin rows with widths <= 9 run the segmented S/N
+    (one row per lane, 8 column segments, rows in 265-float slots); it gives
+    exactly the S/N of the wrapped-window path (feature bit kConeSnrSeg off:
+    RIPTIDE_AMD_CONE_FLAGS=7) and of the single-trial run, and the strict C
+    oracle's at test_full_config_every_row's tolerance, on a multi-pass schedule:
+    the standard ladder, unsorted and non-ladder widths (5, 7, 8), a single
+    width, and rows of 240 bins (24 slack columns) up to 264 (none)."""
+    import torch
+    from riptide_amd import engine, libcpp
+    n, tsamp = 1 << 19, 256e-6
+    x = np.stack([inputs.with_signal(n, tsamp, s, 0.53, 7.0) for s in range(3)])
+    d = torch.from_numpy(x).cuda()
+    out = {}
+    for v in ("15", "7"):
+        monkeypatch.setenv("RIPTIDE_AMD_CONE_FLAGS", v)
+        if widths is None:
+            plan = engine.PeriodogramPlan.for_search(n, tsamp, 0.2, 5.0, bins[0], bins[1], ducy_max=0.05)
+        else:
+            plan = engine.PeriodogramPlan(n, tsamp, widths, 0.2, 5.0, bins[0], bins[1])
+        out[v] = plan.run(d).cpu().numpy()
+    monkeypatch.delenv("RIPTIDE_AMD_CONE_FLAGS")
+    assert np.array_equal(out["15"], out["7"])
+    w = [int(v) for v in plan.widths]
+    _, _, single = libcpp.periodogram(x[2], tsamp, np.asarray(w, dtype=np.uint64), 0.2, 5.0, bins[0], bins[1])
+    assert np.array_equal(out["15"][2], single)
+    _, _, osnr = oracle.periodogram(x[2], tsamp, np.asarray(w, dtype=np.uint64), 0.2, 5.0, bins[0], bins[1],
+                                    threads=min(16, os.cpu_count() or 1))
+    ok, msg = snr_close(out["15"][2], osnr, rtol=2e-6)
+    assert ok, msg
+
+
 def test_fused_ladder_matches_per_rung(monkeypatch):
     """The fused downsampling ladder (one read of the series for every rung)
     produces exactly the per-rung kernel's leaves, hence identical S/N."""

@@ -65,7 +65,7 @@ do_pmc() {     # $1: cfg2 (bench.py, 2 trials) or a config name (tools/ab_flags.
         || fail "pmc pass $i" "$d/p$i.log"
     else
       (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace -f csv -d "$d/p$i" -o run \
-         -- python3 "$R/tools/ab_flags.py" 7 "$cfg" > "$d/p$i.log" 2>&1) || fail "pmc pass $i" "$d/p$i.log"
+         -- python3 "$R/tools/ab_flags.py" 15 "$cfg" > "$d/p$i.log" 2>&1) || fail "pmc pass $i" "$d/p$i.log"
     fi
   done
   local out=profiles/${TAG}_pmc_cone.json
@@ -91,7 +91,7 @@ do_ab() {      # CFG LIB...
   for rep in 1 2; do
     for lib in "$@"; do
       local r
-      r=$(RIPTIDE_AMD_LIB=$lib timeout -k 10 300 python -u tools/ab_env.py "${AB_VAR:-RIPTIDE_AMD_CONE_FLAGS}" "${AB_FLAGS:-7}" "$cfg" 2>&1 | grep '"round": 1') \
+      r=$(RIPTIDE_AMD_LIB=$lib timeout -k 10 300 python -u tools/ab_env.py "${AB_VAR:-RIPTIDE_AMD_CONE_FLAGS}" "${AB_FLAGS:-15}" "$cfg" 2>&1 | grep '"round": 1') \
         || { echo "$lib failed"; exit 1; }
       echo "$r" | sed "s|^|$(basename "$lib") |" | tee -a "$O/ab_$cfg.log"
     done
@@ -166,7 +166,7 @@ PY
   done
 }
 
-do_pmclib() {   # CFG LIB...: the SQ counter groups of the cone kernel per library (tools/ab_flags.py, flags 7)
+do_pmclib() {   # CFG LIB...: the SQ counter groups of the cone kernel per library (tools/ab_flags.py, default flags 15)
   local cfg=$1; shift
   for lib in "$@"; do
     local n=$(basename "$lib" .so) i=0
@@ -174,7 +174,7 @@ do_pmclib() {   # CFG LIB...: the SQ counter groups of the cone kernel per libra
       i=$((i+1))
       local d="$O/pmclib_${cfg}_${n}_p$i"
       (cd /tmp && export TMPDIR=/tmp && RIPTIDE_AMD_LIB=$R/$lib timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace -f csv \
-         -d "$d" -o run -- python3 "$R/tools/ab_flags.py" 7 "$cfg" > "$d.log" 2>&1) || fail "pmclib $n $i" "$d.log"
+         -d "$d" -o run -- python3 "$R/tools/ab_flags.py" 15 "$cfg" > "$d.log" 2>&1) || fail "pmclib $n $i" "$d.log"
     done
     python3 - "$O" "pmclib_${cfg}_${n}" <<'PY'
 import csv, glob, sys
