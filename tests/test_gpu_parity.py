@@ -347,16 +347,21 @@ def test_wide_snr_matches_window_path(monkeypatch, ducy_max, widths):
     assert np.array_equal(out["1"][1], single)
 
 
-@pytest.mark.parametrize("widths, bins", [(None, (240, 260)), ([9, 3, 1], (240, 265)), ([1, 5, 7, 8], (240, 265)),
-                                          ([2], (250, 265))])
+@pytest.mark.parametrize("widths, bins", [(0.05, (240, 260)), (0.2, (240, 260)), ([9, 3, 1], (240, 265)),
+                                          ([1, 5, 7, 8], (240, 265)), ([2], (250, 265)),
+                                          ([120, 1, 2, 5, 13, 40, 77, 91, 215], (240, 265)),
+                                          ([10, 11, 12, 13, 14, 15, 16, 17, 18, 2], (240, 262))])
 def test_segmented_snr_matches_window_path(oracle, monkeypatch, widths, bins):
     """Final units of 240-264-bin rows with widths <= 9 run the segmented S/N
-    (one row per lane, 8 column segments, rows in 265-float slots); it gives
+    (one row per lane, 8 column segments, rows in 265-float slots; plans with
+    a wider width keep the window path, measured faster for them, r05y); it
+    gives
     exactly the S/N of the wrapped-window path (feature bit kConeSnrSeg off:
     RIPTIDE_AMD_CONE_FLAGS=7) and of the single-trial run, and the strict C
     oracle's at test_full_config_every_row's tolerance, on a multi-pass schedule:
-    the standard ladder, unsorted and non-ladder widths (5, 7, 8), a single
-    width, and rows of 240 bins (24 slack columns) up to 264 (none)."""
+    the standard ladders of ducy_max 0.05 and 0.2, unsorted and non-ladder
+    widths (5, 7, 8), a single width, widths up to 215, and rows of 240 bins
+    (24 slack columns) up to 264 (none)."""
     import torch
     from riptide_amd import engine, libcpp
     n, tsamp = 1 << 19, 256e-6
@@ -365,8 +370,8 @@ def test_segmented_snr_matches_window_path(oracle, monkeypatch, widths, bins):
     out = {}
     for v in ("15", "7"):
         monkeypatch.setenv("RIPTIDE_AMD_CONE_FLAGS", v)
-        if widths is None:
-            plan = engine.PeriodogramPlan.for_search(n, tsamp, 0.2, 5.0, bins[0], bins[1], ducy_max=0.05)
+        if isinstance(widths, float):
+            plan = engine.PeriodogramPlan.for_search(n, tsamp, 0.2, 5.0, bins[0], bins[1], ducy_max=widths)
         else:
             plan = engine.PeriodogramPlan(n, tsamp, widths, 0.2, 5.0, bins[0], bins[1])
         out[v] = plan.run(d).cpu().numpy()
