@@ -2652,7 +2652,9 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
     int qout = p;
     // the segmented S/N (snr_segments): rows of 240-264 bins, widths <= 9,
     // <= 64 rows in slots of kSnrSegStride floats (feature bit kConeSnrSeg)
-    const bool seg_snr = SNR && resolved_slots(SMAX) && (a.flags & kConeSnrSeg) && L > 0 && C.slots &&
+    // (not in the WIDE instances: widths past kSnrWin exclude it, and their
+    // code stays free of its registers)
+    const bool seg_snr = SNR && !WIDE && resolved_slots(SMAX) && (a.flags & kConeSnrSeg) && L > 0 && C.slots &&
                          snr_seg_ok(p, wl[kMaxWidths], n0);
     // short rows keep their blob's LDS part at the end of the level buffer,
     // which a final pass's output level (at the S/N stride) and its S/N's
@@ -2727,7 +2729,7 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
             }
         } else if constexpr (SNR) {
             if (seg_snr) {
-                if constexpr (resolved_slots(SMAX))
+                if constexpr (resolved_slots(SMAX) && !WIDE)
                     if (!(a.flags & kConeDiagNoSnr)) snr_segments<SMAX>(a, C.U, buf, wl, n0, tid, whb);
             } else {
 #ifdef RT_STAMPS

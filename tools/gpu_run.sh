@@ -111,7 +111,7 @@ do_flags() {   # CFG FLAGS...
 
 do_stamps() {
   local cfg=${1:-cfg2}
-  RIPTIDE_AMD_LIB=riptide_amd/libriptide_amd_stamps.so timeout -k 10 300 python -u tools/diag_stamps.py 4 "$cfg" \
+  RIPTIDE_AMD_LIB=riptide_amd/libriptide_amd_stamps.so timeout -k 10 300 python -u tools/diag_stamps.py "${STAMPS_B:-4}" "$cfg" \
     > "$O/stamps_$cfg.json" 2> "$O/stamps_$cfg.err" || fail "stamps $cfg" "$O/stamps_$cfg.err"
   cut -c1-1500 "$O/stamps_$cfg.json"
 }
