@@ -462,12 +462,33 @@ __global__ __launch_bounds__(256) void deredden_slope_kernel(const float* __rest
     out += (uint64_t)blockIdx.y * out_stride;
     if (i0 + 4 <= n) {
         const float4 v = *reinterpret_cast<const float4*>(x + i0);
-        float4 r;
-        r.x = (float)__dsub_rn((double)v.x, np_interp_fast(i0, fp, slope, n_lo, factor));
-        r.y = (float)__dsub_rn((double)v.y, np_interp_fast(i0 + 1, fp, slope, n_lo, factor));
-        r.z = (float)__dsub_rn((double)v.z, np_interp_fast(i0 + 2, fp, slope, n_lo, factor));
-        r.w = (float)__dsub_rn((double)v.w, np_interp_fast(i0 + 3, fp, slope, n_lo, factor));
-        *reinterpret_cast<float4*>(out + i0) = r;
+        // the segment of sample i0 from a float estimate corrected by the
+        // exact double tests (np_interp_fast's own loops), then carried to
+        // i0 + 1 .. i0 + 3 (factor >= 2: at most one segment step each)
+        const double c = 0.5 * ((double)factor - 1.0);
+        auto xp = [&](uint32_t j) { return (double)(j * factor) + c; };
+        const uint32_t last = n_lo - 1;
+        const float est = ((float)(2u * i0 + 1u) - (float)factor) / (float)(2u * factor);
+        uint32_t j = est > 0.0f ? min((uint32_t)est, last) : 0u;
+        float rr[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const double xv = (double)(i0 + t);
+            double y;
+            if (xv < c) {
+                y = (double)fp[0];
+            } else if (xv > xp(last)) {
+                y = (double)fp[last];
+            } else {
+                while (j > 0 && xp(j) > xv) --j;
+                while (j < last && xp(j + 1) <= xv) ++j;
+                y = (j == last || xp(j) == xv) ? (double)fp[j]
+                                               : __dadd_rn(__dmul_rn(slope[j], __dsub_rn(xv, xp(j))), (double)fp[j]);
+            }
+            const float xs = t == 0 ? v.x : t == 1 ? v.y : t == 2 ? v.z : v.w;
+            rr[t] = (float)__dsub_rn((double)xs, y);
+        }
+        *reinterpret_cast<float4*>(out + i0) = make_float4(rr[0], rr[1], rr[2], rr[3]);
     } else {
         for (uint32_t i = i0; i < n; ++i) out[i] = (float)__dsub_rn((double)x[i], np_interp_fast(i, fp, slope, n_lo, factor));
     }
@@ -585,6 +606,53 @@ __global__ __launch_bounds__(kNormBlock) void norm_partial_kernel(const float* _
     if (threadIdx.x == 0) partials[(uint64_t)blockIdx.y * gridDim.x + blockIdx.x] = t;
 }
 
+// norm_partial_kernel with 16-byte loads, two per iteration (16-byte aligned
+// rows): the same float64 sums in another order (a per-thread order; numpy's
+// pairwise order is matched by neither, the tests hold the result to 2e-6).
+__global__ __launch_bounds__(kNormBlock) void norm_partial4_kernel(const float* __restrict__ x, uint64_t n,
+                                                                   uint64_t x_stride, double* __restrict__ partials,
+                                                                   const double* __restrict__ stats, int mode)
+{
+    __shared__ double sh[4];
+    x += (uint64_t)blockIdx.y * x_stride;
+    const double mean = mode ? stats[2 * blockIdx.y] : 0.0;
+    double a0 = 0.0, a1 = 0.0;
+    const uint64_t n4 = n >> 2;
+    const uint64_t step = (uint64_t)gridDim.x * kNormBlock;
+    auto add4 = [&](const float4 v, double& acc) {
+        const double e[4] = {(double)v.x, (double)v.y, (double)v.z, (double)v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (mode) {
+                const double d = e[k] - mean;
+                acc += d * d;
+            } else {
+                acc += e[k];
+            }
+        }
+    };
+    uint64_t i = (uint64_t)blockIdx.x * kNormBlock + threadIdx.x;
+    for (; i + step < n4; i += 2 * step) {
+        const float4 v0 = reinterpret_cast<const float4*>(x)[i];
+        const float4 v1 = reinterpret_cast<const float4*>(x)[i + step];
+        add4(v0, a0);
+        add4(v1, a1);
+    }
+    if (i < n4) add4(reinterpret_cast<const float4*>(x)[i], a0);
+    // the n mod 4 tail: block 0
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+        const double v = (double)x[4 * n4 + threadIdx.x];
+        if (mode) {
+            const double d = v - mean;
+            a1 += d * d;
+        } else {
+            a1 += v;
+        }
+    }
+    const double t = block_sum_d(a0 + a1, sh);
+    if (threadIdx.x == 0) partials[(uint64_t)blockIdx.y * gridDim.x + blockIdx.x] = t;
+}
+
 __global__ __launch_bounds__(kNormBlock) void norm_finalize_kernel(const double* __restrict__ partials, uint32_t nblocks,
                                                                    uint64_t n, double* __restrict__ stats, int mode)
 {
@@ -637,9 +705,14 @@ hipError_t launch_normalise(const float* x, uint64_t n, float* out, double* d_pa
 {
     if (!n || !batch) return hipSuccess;
     double* stats = d_partials + (uint64_t)batch * nblocks;
+    const bool vec_in = ((uintptr_t)x % 16) == 0 && x_stride % 4 == 0 && !std::getenv("RIPTIDE_AMD_NORM_SCALAR");
     for (int mode = 0; mode < 2; ++mode) {
-        hipLaunchKernelGGL(norm_partial_kernel, dim3(nblocks, batch), dim3(kNormBlock), 0, s, x, n, x_stride,
-                           d_partials, stats, mode);
+        if (vec_in)
+            hipLaunchKernelGGL(norm_partial4_kernel, dim3(nblocks, batch), dim3(kNormBlock), 0, s, x, n, x_stride,
+                               d_partials, stats, mode);
+        else
+            hipLaunchKernelGGL(norm_partial_kernel, dim3(nblocks, batch), dim3(kNormBlock), 0, s, x, n, x_stride,
+                               d_partials, stats, mode);
         hipLaunchKernelGGL(norm_finalize_kernel, dim3(batch), dim3(kNormBlock), 0, s, d_partials, nblocks, n,
                            stats, mode);
     }

@@ -15,6 +15,8 @@
 
 namespace rt {
 
+template <int N> struct IntC { static constexpr int value = N; };
+
 // ---------------------------------------------------------------------------
 // Downsampling ladder (downsample.hpp:44-82; periodogram.hpp:162-168)
 // ---------------------------------------------------------------------------
@@ -157,6 +159,37 @@ __global__ __launch_bounds__(256) void downsample_fused_kernel(
     __syncthreads();
     const double last = (double)n_in - 1.0;
     const uint32_t b0 = (uint32_t)s0;
+    // one output k of a rung of factor f: window_sum or, with CC > 0 (f <
+    // CC), the window's reads w[0 .. CC) at immediate offsets, the ones past
+    // cnt - 1 adding -0.0 (an exact no-op), instead of window_sum's groups of
+    // eight (at f ~ 1.5, most of the ladder's outputs: 8 reads, selects and
+    // adds for 1-2 terms).  cnt <= floor(f) + 1: reads w[0 .. floor(f)],
+    // inside the staged margin (kDsFusedMargin >= ceil(f) + 2).
+    auto output = [&](auto cc, double f, uint32_t k) -> float {
+        constexpr int CC = decltype(cc)::value;
+        const double start = __dmul_rn((double)k, f);
+        const double end = __dadd_rn(start, f);
+        const double fs = floor(start);
+        double dmax = floor(end);
+        if (dmax > last) dmax = last;
+        const uint32_t imin = (uint32_t)fs, imax = (uint32_t)dmax;
+        const float wmin = (float)__dsub_rn(__dadd_rn(fs, 1.0), start);
+        const float wmax = (float)__dsub_rn(end, dmax);
+        const float* w = span + (imin - b0);
+        const uint32_t cnt = imax - imin;
+        float acc;
+        if constexpr (CC > 0) {
+            float v[CC];
+#pragma unroll
+            for (int j = 0; j < CC; ++j) v[j] = w[j];
+            acc = __fmul_rn(wmin, v[0]);
+#pragma unroll
+            for (int j = 1; j < CC; ++j) acc = __fadd_rn(acc, (uint32_t)j < cnt ? v[j] : -0.0f);
+        } else {
+            acc = window_sum(w, wmin, cnt);
+        }
+        return __fadd_rn(acc, __fmul_rn(wmax, w[cnt]));
+    };
     for (uint32_t ri = 0; ri < num_rungs; ++ri) {
         const DsRung r = rungs[ri];
         float* o = out + r.out_off;
@@ -167,18 +200,22 @@ __global__ __launch_bounds__(256) void downsample_fused_kernel(
             continue;
         }
         const double f = r.f;
-        for (uint32_t k = k_lo + threadIdx.x; k < k_hi; k += 256) {
-            const double start = __dmul_rn((double)k, f);
-            const double end = __dadd_rn(start, f);
-            const double fs = floor(start);
-            double dmax = floor(end);
-            if (dmax > last) dmax = last;
-            const uint32_t imin = (uint32_t)fs, imax = (uint32_t)dmax;
-            const float wmin = (float)__dsub_rn(__dadd_rn(fs, 1.0), start);
-            const float wmax = (float)__dsub_rn(end, dmax);
-            const float* w = span + (imin - b0);
-            const uint32_t cnt = imax - imin;
-            o[k] = __fadd_rn(window_sum(w, wmin, cnt), __fmul_rn(wmax, w[cnt]));
+        auto rung = [&](auto cc) {
+            for (uint32_t k = k_lo + threadIdx.x; k < k_hi; k += 256) o[k] = output(cc, f, k);
+        };
+        switch ((int)f + 1) {
+        case 2: rung(IntC<2>{}); break;
+        case 3: rung(IntC<3>{}); break;
+        case 4: rung(IntC<4>{}); break;
+        case 5: rung(IntC<5>{}); break;
+        case 6: rung(IntC<6>{}); break;
+        case 7: rung(IntC<7>{}); break;
+        case 8: rung(IntC<8>{}); break;
+        case 9: rung(IntC<9>{}); break;
+        case 10: rung(IntC<10>{}); break;
+        case 11: rung(IntC<11>{}); break;
+        case 12: rung(IntC<12>{}); break;
+        default: rung(IntC<0>{}); break;
         }
     }
 }
@@ -1382,7 +1419,6 @@ __device__ __forceinline__ void pack_rolled_lut(lds_cptr sp, int o, unsigned lon
 // kPackLutI: entry x = s + roll (x < p + SEGS) holds the byte offsets
 // 4 ((x + SEGS * e) mod p), e < 8.  The HBM-bound last step of a merge-only
 // pass keeps the contiguous tasks (16-byte stores).
-template <int N> struct IntC { static constexpr int value = N; };
 constexpr int kPackLutI = 128;                // word offset: past the contiguous table's 4p <= 128 words
 static_assert(kPackLutI + 2 * (32 + 4) <= kAuxWords, "short-row roll tables");
 
