@@ -17,8 +17,9 @@
 #   bash tools/gpu_run.sh TAG pmclib CFG LIB...      SQ counter groups of the cone kernel per library
 #   bash tools/gpu_run.sh TAG pmcflags CFG FLAGS...  instruction counters per RIPTIDE_AMD_CONE_FLAGS value
 #                                                    (diagnostic bits: phase attribution of VALU / SALU / LDS)
-#   bash tools/gpu_run.sh TAG round                  round-end pass: pmc (cfg2, cfg3, cfg4), tests, smoke,
-#                                                    bench cfg2 / cfg3 / cfg5, configs, prof
+#   bash tools/gpu_run.sh TAG attrib [CFG]           phase attribution (fill / merge / S/N / skeleton alone)
+#   bash tools/gpu_run.sh TAG round                  round-end pass: attribution (cfg2), pmc (cfg2, cfg3, cfg4),
+#                                                    tests, smoke, bench cfg2 / cfg3 / cfg5, configs, prof
 set -o pipefail
 TAG=$1; CMD=$2; shift 2
 R=$(pwd)
@@ -52,6 +53,10 @@ do_prof() {
      -- python3 "$R/bench.py" --no-cpu-baseline --no-self-check > "$O/bench_prof.log" 2>&1) || fail rocprof "$O/bench_prof.log"
   tail -1 "$O/bench_prof.log" | cut -c1-300
   find "$O/prof" -name '*stats*'
+  python3 tools/prof_json.py "$O/prof/run_kernel_stats.csv" "$O/bench_prof.log" "profiles/${TAG}_kernel_trace.json" \
+    > "$O/prof_json.log" 2>&1 || fail prof_json "$O/prof_json.log"
+  cp "profiles/${TAG}_kernel_trace.json" "$O/"
+  cut -c1-400 "$O/prof_json.log"
 }
 
 do_pmc() {     # $1: cfg2 (bench.py, 2 trials) or a config name (tools/ab_flags.py, 64 trials)
@@ -166,6 +171,14 @@ PY
   done
 }
 
+do_attrib() {   # CFG: phase attribution (tools/attribution.py) -> profiles/TAG_attribution_CFG.json
+  local cfg=${1:-cfg2}
+  timeout -k 10 400 python -u tools/attribution.py "$cfg" "profiles/${TAG}_attribution_$cfg.json" \
+    > "$O/attrib_$cfg.log" 2>&1 || fail "attrib $cfg" "$O/attrib_$cfg.log"
+  cp "profiles/${TAG}_attribution_$cfg.json" "$O/"
+  tail -1 "$O/attrib_$cfg.log" | cut -c1-600
+}
+
 do_pmclib() {   # CFG LIB...: the SQ counter groups of the cone kernel per library (tools/ab_flags.py, default flags 15)
   local cfg=$1; shift
   for lib in "$@"; do
@@ -203,7 +216,9 @@ case "$CMD" in
   parity) do_parity "$@" ;;
   pmcflags) do_pmcflags "$@" ;;
   pmclib) do_pmclib "$@" ;;
+  attrib) do_attrib "$@" ;;
   round)
+    RIPTIDE_AMD_SCRATCH_MFLOATS=1536 do_attrib cfg2
     do_pmc cfg2
     do_pmc cfg3
     do_pmc cfg4
