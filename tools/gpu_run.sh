@@ -206,6 +206,8 @@ PY
 case "$CMD" in
   tests) do_tests ;;
   bench) do_bench bench "$@" ;;
+  bench3) do_bench bench_cfg3 --workload cfg3 "$@" ;;
+  bench5) do_bench bench_cfg5 --workload cfg5 "$@" ;;
   prof) do_prof ;;
   pmc) do_pmc "${1:-cfg2}" ;;
   configs) do_configs "$@" ;;
