@@ -306,14 +306,14 @@ def self_check(torch, dist, engine, plan, xbuf, snr, c, local, world, dev):
     the library's default transform grouping (96 Mi floats per buffer: the
     schedule every GPU parity test runs); True on every rank only if its S/N
     is bit-identical to the benchmarked schedule's (snr[0])."""
-    saved = os.environ.get("RIPTIDE_AMD_SCRATCH_MFLOATS")
-    os.environ.pop("RIPTIDE_AMD_SCRATCH_MFLOATS", None)
+    saved = {k: os.environ.pop(k, None) for k in ("RIPTIDE_AMD_SCRATCH_MFLOATS", "RIPTIDE_AMD_COSCHED")}
     try:
         ref = engine.PeriodogramPlan.for_search(c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"],
                                                 ducy_max=c["ducy_max"], device=local)
     finally:
-        if saved is not None:
-            os.environ["RIPTIDE_AMD_SCRATCH_MFLOATS"] = saved
+        for k, v in saved.items():
+            if v is not None:
+                os.environ[k] = v
     got = ref.run(xbuf[0:1].contiguous(), check=True)
     torch.cuda.synchronize()
     same = bool(torch.equal(got[0], snr[0]))
@@ -476,9 +476,17 @@ def main():
     # workspace at 16 trials (53 GB at 384 M), so only where it fits: one
     # workspace, one rank per GPU, and enough free HBM (checked below); cfg3
     # at 32 trials has few launches at 384 M already
+    # Round 5: two 1024 M-float groups co-scheduled on two streams
+    # (RIPTIDE_AMD_COSCHED=1: group g's merge-only passes run beside group
+    # g - 1's S/N passes) for the same workspace as one 1536 M group: cfg2
+    # cone 6.208-6.215 -> 6.160-6.169 ms per trial (profiles/r05zl_*.log)
     user_scratch = "RIPTIDE_AMD_SCRATCH_MFLOATS" in os.environ
+    user_cosched = "RIPTIDE_AMD_COSCHED" in os.environ
     if args.workload in ("cfg2", "cfg3"):
         big = args.workload == "cfg2" and not args.overlap and not args.one_gpu_rehearsal
+        if big and not user_scratch and not user_cosched:
+            os.environ["RIPTIDE_AMD_COSCHED"] = "1"
+            os.environ["RIPTIDE_AMD_SCRATCH_MFLOATS"] = "1024"
         os.environ.setdefault("RIPTIDE_AMD_SCRATCH_MFLOATS", "1536" if big else "384")
     import torch
     import torch.distributed as dist
@@ -514,6 +522,8 @@ def main():
         need = plan.workspace_bytes(B) + 4 * B * (plan.length * plan.num_widths + 3 * c["n"])
         if need > 0.9 * torch.cuda.mem_get_info(dev)[0]:
             os.environ["RIPTIDE_AMD_SCRATCH_MFLOATS"] = "384"
+            if not user_cosched:
+                os.environ.pop("RIPTIDE_AMD_COSCHED", None)
             del plan
             plan = engine.PeriodogramPlan.for_search(c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"],
                                                      c["bmax"], ducy_max=c["ducy_max"], device=local)
@@ -610,6 +620,7 @@ def main():
                 "ffa_transforms": stats["transforms"],
                 "cone_launches_per_step": stats["launches"],
                 "scratch_mfloats_per_buffer_trial": float(os.environ["RIPTIDE_AMD_SCRATCH_MFLOATS"]),
+                "cosched_groups": os.environ.get("RIPTIDE_AMD_COSCHED") == "1",
                 "streams": "prep (deredden+normalise+ladder of step k+1) || FFA passes of step k" if args.overlap
                            else "one",
                 "parallelism": f"dm-trials x{world} (independent, weak scaling)" + REHEARSAL,

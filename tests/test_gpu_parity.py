@@ -483,15 +483,18 @@ def test_bench_schedule_cfg2(rt, golden_full, monkeypatch):
     _check_full_snrs(rt, g, c, one, periods, foldbins, got[0].cpu().numpy())
 
 
-@pytest.mark.parametrize("name,budget", [("cfg2", "1536"), ("cfg4", None), ("cfg1", None), ("cfg3", "384")])
-def test_full_config_every_row(rt, oracle, golden_full, monkeypatch, name, budget):
+@pytest.mark.parametrize("name,budget,cosched", [("cfg2", "1024", True), ("cfg2", "1536", False),
+                                                 ("cfg4", None, False), ("cfg1", None, False),
+                                                 ("cfg3", "384", False)])
+def test_full_config_every_row(rt, oracle, golden_full, monkeypatch, name, budget, cosched):
     """Every one of the L x W S/N values at full size (missing 3):
     the golden input through the schedule bench.py times for the config,
     compared element by element with the strict C oracle run on the same
     dereddened, normalised series (periodogram.hpp:175-194; threaded, same
     arithmetic per step) at the 2e-6 scaled tolerance of
     test_periodogram_golden, and with the golden sampled rows / sums / peaks
-    of the reference build at 1e-4."""
+    of the reference build at 1e-4.  cfg2 at 1024 M co-scheduled is
+    bench.py's schedule since round 5, at 1536 M its round-4 one."""
     import torch
     from riptide_amd import engine
     g = golden_full["configs"][name]
@@ -501,6 +504,8 @@ def test_full_config_every_row(rt, oracle, golden_full, monkeypatch, name, budge
         pytest.fail(f"input generator drifted on this host: input sha256 {sha(raw)} != golden {g['input_sha']}")
     if budget:
         monkeypatch.setenv("RIPTIDE_AMD_SCRATCH_MFLOATS", budget)
+    if cosched:
+        monkeypatch.setenv("RIPTIDE_AMD_COSCHED", "1")
     plan = engine.PeriodogramPlan.for_search(c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"],
                                              ducy_max=c["ducy_max"])
     x = engine.deredden_normalise(torch.from_numpy(raw).cuda(), int(round(4.0 / c["tsamp"])), 101)
@@ -539,7 +544,7 @@ def test_single_stream_matches_two_streams_cfg2(rt, golden_full, monkeypatch):
     assert torch.equal(one, two), "single-stream schedule differs from the two-stream chains"
 
 
-@pytest.mark.parametrize("budget", ["384", "96"])
+@pytest.mark.parametrize("budget", ["1024", "384", "96"])
 def test_cosched_schedule_cfg2(rt, golden_full, monkeypatch, budget):
     """Co-scheduled transform groups (RIPTIDE_AMD_COSCHED=1: two scratch
     banks, group g on stream g mod 2, its merge-only launches overlapping

@@ -220,7 +220,7 @@ case "$CMD" in
   pmclib) do_pmclib "$@" ;;
   attrib) do_attrib "$@" ;;
   round)
-    RIPTIDE_AMD_SCRATCH_MFLOATS=1536 do_attrib cfg2
+    RIPTIDE_AMD_SCRATCH_MFLOATS=1024 RIPTIDE_AMD_COSCHED=1 do_attrib cfg2
     do_pmc cfg2
     do_pmc cfg3
     do_pmc cfg4
