@@ -364,6 +364,15 @@ def bench_cfg3(args, torch, dist, world, rank, local, dev):
     B = min(args.batch, max(1, len(mine)))
     plan = engine.PeriodogramPlan.for_search(c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"],
                                              ducy_max=c["ducy_max"], device=local)
+    if os.environ.get("RIPTIDE_AMD_COSCHED") == "1":
+        # two scratch banks only if they, the resident trials and the batch
+        # buffers leave 10 % of the free HBM
+        need = plan.workspace_bytes(B) + 4 * c["n"] * (len(mine) + 3 * B) + 4 * B * plan.length * plan.num_widths
+        if need > 0.9 * torch.cuda.mem_get_info(dev)[0]:
+            os.environ.pop("RIPTIDE_AMD_COSCHED")
+            del plan
+            plan = engine.PeriodogramPlan.for_search(c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"],
+                                                     c["bmax"], ducy_max=c["ducy_max"], device=local)
     ws_samples = int(round(c["rmed_width"] / c["tsamp"]))
     X = cfg3_trials(torch, mine, c["n"], c["tsamp"], dev)
     xbuf = torch.empty((B, c["n"]), dtype=torch.float32, device=dev)
@@ -433,6 +442,8 @@ def bench_cfg3(args, torch, dist, world, rank, local, dev):
                 "trials_total": ntr, "trials_per_gpu": len(mine), "batch": B,
                 "trial_periods": plan.length, "ffa_transforms": stats["transforms"],
                 "cone_launches_per_batch": stats["launches"],
+                "scratch_mfloats_per_buffer_trial": float(os.environ.get("RIPTIDE_AMD_SCRATCH_MFLOATS", "96")),
+                "cosched_groups": os.environ.get("RIPTIDE_AMD_COSCHED") == "1",
                 "parallelism": f"dm-trials x{world} (round-robin shard of one job, strong scaling)" + REHEARSAL,
             },
             "roofline": rf,
@@ -487,6 +498,11 @@ def main():
         if big and not user_scratch and not user_cosched:
             os.environ["RIPTIDE_AMD_COSCHED"] = "1"
             os.environ["RIPTIDE_AMD_SCRATCH_MFLOATS"] = "1024"
+        # cfg3: its 384 M groups co-scheduled too, where the second bank fits
+        # (bench_cfg3): cone 1.645-1.652 -> 1.637-1.639 ms per trial
+        # (profiles/r05zn_ab_cosched_cfg3.log)
+        if args.workload == "cfg3" and not user_cosched and not args.one_gpu_rehearsal:
+            os.environ["RIPTIDE_AMD_COSCHED"] = "1"
         os.environ.setdefault("RIPTIDE_AMD_SCRATCH_MFLOATS", "1536" if big else "384")
     import torch
     import torch.distributed as dist
