@@ -148,8 +148,8 @@ do_pmcflags() {   # CFG FLAGS...
   local cfg=$1; shift
   for f in "$@"; do
     local d="$O/pmcflags_${cfg}_$f"
-    (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS \
-       SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE GRBM_COUNT \
+    (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT \
+       SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE GRBM_COUNT \
        --kernel-trace -f csv -d "$d" -o run -- python3 "$R/tools/ab_flags.py" "$f" "$cfg" > "$d.log" 2>&1) \
       || fail "pmcflags $f" "$d.log"
     python3 - "$d" "$f" <<'PY'
