@@ -2259,25 +2259,28 @@ __device__ __forceinline__ float seg_window_max(const f2v (&P)[K + 5], const f2v
 }
 
 // Segmented boxcar S/N (snr.hpp:37-65, kernels.hpp:50-101) of a final level
-// of 240-264-bin rows, row r at slot + r * kSnrSegStride + r0 (r0 = 8 S - p
-// <= 24 columns of slack in front of the row): lane = row, wave w = slot
-// columns [w S, w S + S).  The slack columns count as +0.0 samples and +inf
-// prefix values (selects in wave 0 only), so they add nothing to the sums and
-// never start a window.  Per block of 64 rows:
-//   A. the segment's samples into registers; their fp64 sum to the exchange
-//      area (kSnrSegExch floats at the end of the level buffer);
-//   B. the segment's offset (the sums of the segments before it, in order)
-//      and the row total; the segment's fp64 running sum, cast per column to
-//      float (circular_prefix_sum, kernels.hpp:62-80); its first 9 prefix
-//      values written back in place (wave 0: all S -- the wrap reads columns
-//      0 .. 8);
-//   C. the next segment's first 9 prefix values (the last segment: the wrap
-//      c[p + e] = c[e] + sum, kernels.hpp:88-97), then every width's window
-//      maximum over the segment's starts, written over the row's slot head;
+// of <= 64 rows of 240-264 bins, row r at slot + r * kSnrSegStride + r0 (r0 =
+// 8 S - p <= 24 columns of slack in front of the row): lane = row, wave w =
+// slot columns [w S, w S + S).  The slack columns count as +0.0 samples and
+// +inf prefix values (selects in wave 0 only), so they add nothing to the
+// sums and never start a window.
+//   A. the segment's S samples and the next segment's first E (the last
+//      segment: the row's first E) into registers; the segment's fp64 sum to
+//      the exchange area (kSnrSegExch floats at the end of the level buffer);
+//   B. the segment's offset (the sums of the segments before it, in order),
+//      the row total, the segment's fp64 running sum cast per column
+//      (circular_prefix_sum, kernels.hpp:62-80), and the next segment's first
+//      E prefix values the same way from offset + this segment's sum -- the
+//      very additions the next wave makes -- (the last segment: the wrap
+//      c[p + e] = c[e] + sum, kernels.hpp:88-97, c[e] from the row's first
+//      samples from +0.0, as wave 0 does);
+//   C. every width's window maximum over the segment's starts, to a maxima
+//      area below the exchange area (the rows' samples are all in registers
+//      by then: the phase-A barrier);
 //   D. width iw on wave iw (mod 8): the 8 segment maxima, the S/N formula,
 //      one store per row.
-// Each lane works on its own row throughout: no cross-lane shuffles or
-// scans, 4 workgroup barriers per 64 rows.
+// Each lane works on its own row throughout: no shuffles or scans, and no
+// prefix values exchanged (2 workgroup barriers).
 template <int SMAX>
 __device__ __forceinline__ void snr_segments(const ConeArgs& a, const UnitView& U, float* slot, const int* wl,
                                              int nrows, int tid, const float* whb)
@@ -2286,7 +2289,9 @@ __device__ __forceinline__ void snr_segments(const ConeArgs& a, const UnitView& 
     constexpr int E = kSnrSegWmax;
     constexpr int K = S / 2;
     constexpr int q = kSnrSegStride;
+    constexpr int kMax = 8 * E * 64;          // maxima area: [segment][width - 1][lane]
     static_assert(S == 2 * K + 1 && 2 * (K + 5) >= S + E && 8 * S - 24 > 0, "segment shape");
+    static_assert(kSnrSegRows <= 64 && kLdsBufFloats - kSnrSegExch - kMax >= 0, "segmented S/N areas");
     // an opaque thread index (as snr_epilogue)
     asm volatile("" : "+v"(tid));
     const int lane = tid & 63;
@@ -2303,123 +2308,123 @@ __device__ __forceinline__ void snr_segments(const ConeArgs& a, const UnitView& 
     uint32_t wmask = 0;
     for (uint32_t iw = 0; iw < nw; ++iw) wmask |= 1u << uni(wl[iw]);
     double* const exch = reinterpret_cast<double*>(slot + kLdsBufFloats - kSnrSegExch);
+    float* const maxa = slot + kLdsBufFloats - kSnrSegExch - kMax;
     float* const snr = a.snr + (uint64_t)U.trial * a.snr_stride + (U.snr_row + (uint64_t)U.s0) * (uint64_t)nw;
     const __amdgpu_buffer_rsrc_t srs = buffer_rsrc(snr, (uint32_t)nev * nw * 4u);
-    for (int rb = 0; rb < nev; rb += 64) {
-        const int r = rb + lane;
-        const bool act = r < nev;
-        // rows past nev compute (and write) the values of row nev - 1 again
-        float* const row = slot + min(r, nev - 1) * q;
-        float* const seg = row + wave * S;
-        float c[S];
-        // A: samples and the segment sum
+    // one block of <= 64 rows (snr_seg_ok); rows past nev compute the values
+    // of row nev - 1 again and do not store
+    const int r = lane;
+    const bool act = r < nev;
+    float* const row = slot + min(r, nev - 1) * q;
+    const float* const seg = row + wave * S;
+    float c[S], n[E];
+    // A: samples (this segment, then the next one's first E) and the sum
 #pragma unroll
-        for (int g = 0; g < S; ++g) c[g] = lds_ld((lds_cptr)(seg + g));
-        if (wave == 0) {
-            asm volatile("" : "+v"(r0v));     // per block: the compares stay in place
+    for (int g = 0; g < S; ++g) c[g] = lds_ld((lds_cptr)(seg + g));
+    {
+        const lds_cptr nx = (lds_cptr)(wave < 7 ? seg + S : row + r0);
 #pragma unroll
-            for (int g = 0; g < 24; ++g) c[g] = g < r0v ? 0.0f : c[g];
+        for (int e = 0; e < E; ++e) n[e] = lds_ld(nx + e);
+    }
+    if (wave == 0) {
+        asm volatile("" : "+v"(r0v));
+#pragma unroll
+        for (int g = 0; g < 24; ++g) c[g] = g < r0v ? 0.0f : c[g];
+    }
+    // (the first addition of 0.0 dropped: a -0.0 sum is made +0.0 by the
+    // offsets' and the total's +0.0 starts)
+    double part = (double)c[0];
+#pragma unroll
+    for (int g = 1; g < S; ++g) part = part + (double)c[g];
+    exch[wave * 64 + lane] = part;
+    lds_barrier();
+    // B: offset, total, prefix values of this segment and of the next one's
+    // first E columns
+    double off = 0.0, tot = 0.0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        const double pv = exch[w * 64 + lane];
+        if (w < wave) off = off + pv;
+        tot = tot + pv;
+    }
+    const float sumx = (float)tot;
+    double acc = off;
+#pragma unroll
+    for (int g = 0; g < S; ++g) {
+        acc = acc + (double)c[g];
+        c[g] = (float)acc;
+    }
+    {
+        // the next wave's offset is ((p_0 + p_1) + ...) + p_wave: off + part,
+        // the same additions; the last wave starts the row over from +0.0
+        double an = wave < 7 ? off + part : 0.0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            an = an + (double)n[e];
+            n[e] = (float)an;
         }
-        // (the first addition of 0.0 dropped: a -0.0 sum is made +0.0 by
-        // the offsets' and the total's +0.0 starts)
-        double part = (double)c[0];
+        if (wave == 7) {
 #pragma unroll
-        for (int g = 1; g < S; ++g) part = part + (double)c[g];
-        exch[wave * 64 + lane] = part;
-        lds_barrier();
-        // B: offset, total, prefix values
-        double off = 0.0, tot = 0.0;
-#pragma unroll
-        for (int w = 0; w < 8; ++w) {
-            const double pv = exch[w * 64 + lane];
-            if (w < wave) off = off + pv;
-            tot = tot + pv;
+            for (int e = 0; e < E; ++e) n[e] = __fadd_rn(n[e], sumx);
         }
-        const float sumx = (float)tot;
-        double acc = off;
+    }
+    // C: the window maxima; prefix values as pairs P[k] = c[2k], c[2k + 1]
+    // (wave 0: +inf at the slack starts), c[S + e] = n[e]
+    f2v P[K + 5], H[K + 4];
 #pragma unroll
-        for (int g = 0; g < S; ++g) {
-            acc = acc + (double)c[g];
-            c[g] = (float)acc;
+    for (int k = 0; k < K; ++k) P[k] = f2v{c[2 * k], c[2 * k + 1]};
+    P[K] = f2v{c[2 * K], n[0]};
+#pragma unroll
+    for (int k = K + 1; k < K + 5; ++k) P[k] = f2v{n[2 * (k - K) - 1], n[2 * (k - K)]};
+    if (wave == 0) {
+        asm volatile("" : "+v"(r0v));
+#pragma unroll
+        for (int g = 0; g < 24; ++g) {
+            if (g & 1) P[g / 2].y = g < r0v ? INFINITY : P[g / 2].y;
+            else P[g / 2].x = g < r0v ? INFINITY : P[g / 2].x;
         }
-        if (wave == 0) {
+    }
 #pragma unroll
-            for (int g = 0; g < S; ++g) seg[g] = c[g];
-        } else {
+    for (int k = 0; k < K + 4; ++k) H[k] = f2v{P[k].y, P[k + 1].x};
+    float m[E + 1];
 #pragma unroll
-            for (int g = 0; g < E; ++g) seg[g] = c[g];
-        }
-        lds_barrier();
-        // C: the next segment's first prefix values, the window maxima
-        f2v P[K + 5], H[K + 4];
+    for (int w = 0; w <= E; ++w) m[w] = -INFINITY;
+    constexpr uint32_t kStdMask = (1u << 1) | (1u << 2) | (1u << 3) | (1u << 4) | (1u << 6) | (1u << 9);
+    if (wmask == kStdMask) {
+        // the standard ladder 1, 2, 3, 4, 6, 9 in one block: six independent
+        // max chains for the scheduler to interleave
+        m[1] = seg_window_max<K, 1>(P, H);
+        m[2] = seg_window_max<K, 2>(P, H);
+        m[3] = seg_window_max<K, 3>(P, H);
+        m[4] = seg_window_max<K, 4>(P, H);
+        m[6] = seg_window_max<K, 6>(P, H);
+        m[9] = seg_window_max<K, 9>(P, H);
+    } else {
+        if (wmask & (1u << 1)) m[1] = seg_window_max<K, 1>(P, H);
+        if (wmask & (1u << 2)) m[2] = seg_window_max<K, 2>(P, H);
+        if (wmask & (1u << 3)) m[3] = seg_window_max<K, 3>(P, H);
+        if (wmask & (1u << 4)) m[4] = seg_window_max<K, 4>(P, H);
+        if (wmask & (1u << 5)) m[5] = seg_window_max<K, 5>(P, H);
+        if (wmask & (1u << 6)) m[6] = seg_window_max<K, 6>(P, H);
+        if (wmask & (1u << 7)) m[7] = seg_window_max<K, 7>(P, H);
+        if (wmask & (1u << 8)) m[8] = seg_window_max<K, 8>(P, H);
+        if (wmask & (1u << 9)) m[9] = seg_window_max<K, 9>(P, H);
+    }
 #pragma unroll
-        for (int k = 0; k <= K; ++k) P[k] = f2v{c[2 * k], 2 * k + 1 < S ? c[2 * k + 1] : 0.0f};
-        float n[E];
-        if (wave < 7) {
+    for (int w = 1; w <= E; ++w)
+        if (wmask & (1u << w)) maxa[(wave * E + w - 1) * 64 + lane] = m[w];
+    lds_barrier();
+    // D: width iw on wave iw (mod 8)
+    for (int iw = wave; iw < (int)nw; iw += 8) {
+        const int w = uni(wl[iw]);
+        const lds_cptr mx = (lds_cptr)(maxa + (w - 1) * 64 + lane);
+        float dm = lds_ld(mx);
 #pragma unroll
-            for (int e = 0; e < E; ++e) n[e] = lds_ld((lds_cptr)(seg + S + e));
-        } else {
-            const lds_cptr w0 = (lds_cptr)(row + r0);
-#pragma unroll
-            for (int e = 0; e < E; ++e) n[e] = __fadd_rn(lds_ld(w0 + e), sumx);
-        }
-        // c[S + e] = n[e]: P[K].y, then pairs K + 1 ..
-        P[K].y = n[0];
-#pragma unroll
-        for (int k = K + 1; k < K + 5; ++k) P[k] = f2v{n[2 * (k - K) - 1], n[2 * (k - K)]};
-        if (wave == 0) {
-            asm volatile("" : "+v"(r0v));
-#pragma unroll
-            for (int g = 0; g < 24; ++g) {
-                if (g & 1) P[g / 2].y = g < r0v ? INFINITY : P[g / 2].y;
-                else P[g / 2].x = g < r0v ? INFINITY : P[g / 2].x;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < K + 4; ++k) H[k] = f2v{P[k].y, P[k + 1].x};
-        float m[E + 1];
-#pragma unroll
-        for (int w = 0; w <= E; ++w) m[w] = -INFINITY;
-        constexpr uint32_t kStdMask = (1u << 1) | (1u << 2) | (1u << 3) | (1u << 4) | (1u << 6) | (1u << 9);
-        if (wmask == kStdMask) {
-            // the standard ladder 1, 2, 3, 4, 6, 9 in one block: six
-            // independent max chains for the scheduler to interleave
-            m[1] = seg_window_max<K, 1>(P, H);
-            m[2] = seg_window_max<K, 2>(P, H);
-            m[3] = seg_window_max<K, 3>(P, H);
-            m[4] = seg_window_max<K, 4>(P, H);
-            m[6] = seg_window_max<K, 6>(P, H);
-            m[9] = seg_window_max<K, 9>(P, H);
-        } else {
-            if (wmask & (1u << 1)) m[1] = seg_window_max<K, 1>(P, H);
-            if (wmask & (1u << 2)) m[2] = seg_window_max<K, 2>(P, H);
-            if (wmask & (1u << 3)) m[3] = seg_window_max<K, 3>(P, H);
-            if (wmask & (1u << 4)) m[4] = seg_window_max<K, 4>(P, H);
-            if (wmask & (1u << 5)) m[5] = seg_window_max<K, 5>(P, H);
-            if (wmask & (1u << 6)) m[6] = seg_window_max<K, 6>(P, H);
-            if (wmask & (1u << 7)) m[7] = seg_window_max<K, 7>(P, H);
-            if (wmask & (1u << 8)) m[8] = seg_window_max<K, 8>(P, H);
-            if (wmask & (1u << 9)) m[9] = seg_window_max<K, 9>(P, H);
-        }
-        lds_barrier();                        // every wave is past its reads of the rows
-#pragma unroll
-        for (int w = 1; w <= E; ++w)
-            if (wmask & (1u << w)) row[E * wave + w - 1] = m[w];
-        lds_barrier();
-        // D: width iw on wave iw (mod 8)
-        for (int iw = wave; iw < (int)nw; iw += 8) {
-            const int w = uni(wl[iw]);
-            const lds_cptr mx = (lds_cptr)(row + w - 1);
-            float dm = lds_ld(mx);
-#pragma unroll
-            for (int k = 1; k < 8; ++k) dm = fmaxf(dm, lds_ld(mx + E * k));
-            const float hpb = whb[2 * iw], b = whb[2 * iw + 1];
-            const float v = (hpb * dm - b * sumx) / U.stdnoise;
-            const uint32_t o = act ? ((uint32_t)r * nw + (uint32_t)iw) * 4u : 0x80000000u;
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srs, (int)o, 0, kSnrCpol);
-        }
-        // the next block's phase-A exchange writes come after this block's
-        // phase-B reads (two barriers between); its rows are other rows
+        for (int k = 1; k < 8; ++k) dm = fmaxf(dm, lds_ld(mx + E * 64 * k));
+        const float hpb = whb[2 * iw], b = whb[2 * iw + 1];
+        const float v = (hpb * dm - b * sumx) / U.stdnoise;
+        const uint32_t o = act ? ((uint32_t)r * nw + (uint32_t)iw) * 4u : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), srs, (int)o, 0, kSnrCpol);
     }
 }
 
