@@ -21,7 +21,7 @@ def main():
     flags = sys.argv[1].split(",") if len(sys.argv) > 1 else ["3", "0"]
     c = {k["name"]: k for k in CONFIGS}[sys.argv[2] if len(sys.argv) > 2 else "cfg2"]
     n = c["n"]
-    B = 8
+    B = int(os.environ.get("AB_BATCH", "8"))     # tools/gpu_run.sh pmc: 16, the configs table's batch
     plan = engine.PeriodogramPlan.for_search(n, c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"],
                                              ducy_max=c["ducy_max"])
     x = torch.randn((B, n), device="cuda", dtype=torch.float32)

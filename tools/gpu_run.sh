@@ -69,13 +69,13 @@ do_pmc() {     # $1: cfg2 (bench.py, 2 trials) or a config name (tools/ab_flags.
          -- python3 "$R/bench.py" --steps 1 --warmup 1 --batch 2 --no-cpu-baseline --no-self-check > "$d/p$i.log" 2>&1) \
         || fail "pmc pass $i" "$d/p$i.log"
     else
-      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace -f csv -d "$d/p$i" -o run \
+      (cd /tmp && export TMPDIR=/tmp && export AB_BATCH=16 && timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace -f csv -d "$d/p$i" -o run \
          -- python3 "$R/tools/ab_flags.py" 15 "$cfg" > "$d/p$i.log" 2>&1) || fail "pmc pass $i" "$d/p$i.log"
     fi
   done
   local out=profiles/${TAG}_pmc_cone.json
   [ "$cfg" = cfg2 ] || out=profiles/${TAG}_pmc_cone_$cfg.json
-  local per=4; [ "$cfg" = cfg2 ] || per=64
+  local per=4; [ "$cfg" = cfg2 ] || per=128     # ab_flags.py: 2 rounds x 4 runs x AB_BATCH 16 trials
   python3 tools/pmc_to_json.py "$d" "$out" $per --config "$cfg" > "$d/json.log" 2>&1 || fail pmc_to_json "$d/json.log"
   cp "$out" "$O/"
   echo "pmc $cfg ok: $(head -c 300 "$d/json.log")"
