@@ -365,6 +365,56 @@ __device__ float np_pairwise_sum(const float* a, int n)
     return ret;
 }
 
+// np_pairwise_sum for the counts whose halving tree has one level (n <= 128,
+// or both halves <= 128: np_pairwise_split2), without the general form's
+// explicit stack (private arrays indexed at run time live in scratch memory)
+__host__ __device__ inline bool np_pairwise_split2(int n)
+{
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    return n <= 128 || n - n2 <= 128;
+}
+
+__device__ __forceinline__ float np_pairwise_sum2(const float* a, int n)
+{
+    if (n <= 128) return np_pairwise_leaf(a, n);
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    const float left = np_pairwise_leaf(a, n2);
+    return __fadd_rn(left, np_pairwise_leaf(a + n2, n - n2));
+}
+
+// scrunch_kernel for np_pairwise_split2(factor) <= kScrunchMaxFactor: 64
+// outputs per block, their 64 * factor input samples staged in LDS by the
+// block's four waves with coalesced (16-byte where aligned) loads -- one
+// thread per output reading its own block straight from global memory
+// touched 64 cache lines per load instruction and re-fetched them from L2 --
+// then one lane per output sums its block from LDS in numpy's pairwise order.
+constexpr uint32_t kScrunchMaxFactor = 256;
+
+__global__ __launch_bounds__(256) void scrunch2_kernel(const float* __restrict__ x, uint64_t n_out, uint32_t factor,
+                                                       float* __restrict__ out, uint64_t x_stride, uint64_t out_stride,
+                                                       int vec)
+{
+    extern __shared__ float stage[];
+    const uint64_t i0 = (uint64_t)blockIdx.x * 64;
+    const uint32_t rows = (uint32_t)min<uint64_t>(64, n_out - i0);
+    const uint32_t len = rows * factor;
+    const float* src = x + (uint64_t)blockIdx.y * x_stride + i0 * factor;
+    if (vec) {   // src 16-byte aligned (launch: x, x_stride and 64 * factor)
+        const uint32_t n4 = len / 4;
+        for (uint32_t k = threadIdx.x; k < n4; k += 256)
+            reinterpret_cast<float4*>(stage)[k] = reinterpret_cast<const float4*>(src)[k];
+        for (uint32_t k = 4 * n4 + threadIdx.x; k < len; k += 256) stage[k] = src[k];
+    } else {
+        for (uint32_t k = threadIdx.x; k < len; k += 256) stage[k] = src[k];
+    }
+    __syncthreads();
+    if (threadIdx.x >= rows) return;
+    const float sum = np_pairwise_sum2(stage + threadIdx.x * factor, (int)factor);
+    out[(uint64_t)blockIdx.y * out_stride + i0 + threadIdx.x] = (float)((double)sum / (double)factor);
+}
+
 // scrunch(): mean of consecutive blocks of `factor` samples; numpy divides the
 // float32 sum by an np.intp count, i.e. in float64, then casts to float32.
 __global__ __launch_bounds__(256) void scrunch_kernel(const float* __restrict__ x, uint64_t n_out, uint32_t factor,
@@ -382,8 +432,14 @@ hipError_t launch_scrunch(const float* x, uint64_t n_out, uint32_t factor, float
                           uint64_t out_stride, uint32_t batch, hipStream_t s)
 {
     if (!n_out || !batch) return hipSuccess;
-    hipLaunchKernelGGL(scrunch_kernel, dim3((uint32_t)((n_out + 255) / 256), batch), dim3(256), 0, s,
-                       x, n_out, factor, out, x_stride, out_stride);
+    if (factor <= kScrunchMaxFactor && np_pairwise_split2((int)factor)) {
+        const int vec = ((uintptr_t)x % 16) == 0 && x_stride % 4 == 0 && (64 * factor) % 4 == 0;
+        hipLaunchKernelGGL(scrunch2_kernel, dim3((uint32_t)((n_out + 63) / 64), batch), dim3(256),
+                           64 * factor * sizeof(float), s, x, n_out, factor, out, x_stride, out_stride, vec);
+    }
+    else
+        hipLaunchKernelGGL(scrunch_kernel, dim3((uint32_t)((n_out + 255) / 256), batch), dim3(256), 0, s,
+                           x, n_out, factor, out, x_stride, out_stride);
     return hipGetLastError();
 }
 
@@ -446,51 +502,125 @@ __device__ __forceinline__ double np_interp_fast(uint32_t i, const float* __rest
 }
 
 // out[i] = float32(x[i] - interp(i))  (time_series.py:118-122), the slopes
-// from interp_slope_kernel (factor > 1, n < 2^31)
+// from interp_slope_kernel (factor > 1, n < 2^30).  STATS: the block's sums
+// of out and out^2 in float64 (partials[2 * (y * gridDim.x + x) + {0, 1}])
+// for the normalisation that follows (norm_stats_finalize_kernel), saving
+// its two read passes of the series.
+constexpr uint32_t kDeredGroups = 4;   // deredden_slope_kernel: 16 samples per thread, 4096 per block
+
+template <bool STATS>
 __global__ __launch_bounds__(256) void deredden_slope_kernel(const float* __restrict__ x, uint32_t n,
                                                              const float* __restrict__ fp, const double* __restrict__ slope,
                                                              uint32_t n_lo, uint32_t factor, float* __restrict__ out,
-                                                             uint64_t x_stride, uint64_t lo_stride, uint64_t out_stride)
+                                                             uint64_t x_stride, uint64_t lo_stride, uint64_t out_stride,
+                                                             double* __restrict__ partials)
 {
-    // four consecutive samples per thread: 16-byte loads and stores where the
-    // rows are 16-byte aligned (the launch checks the strides and bases)
-    const uint32_t i0 = 4u * (blockIdx.x * 256u + threadIdx.x);
-    if (i0 >= n) return;
+    // kDeredGroups groups of four consecutive samples per thread (16-byte
+    // loads and stores: the launch checks the strides and bases), the
+    // block's groups interleaved for coalescing
     x += (uint64_t)blockIdx.y * x_stride;
     fp += (uint64_t)blockIdx.y * lo_stride;
     slope += (uint64_t)blockIdx.y * lo_stride;
     out += (uint64_t)blockIdx.y * out_stride;
-    if (i0 + 4 <= n) {
-        const float4 v = *reinterpret_cast<const float4*>(x + i0);
-        // the segment of sample i0 from a float estimate corrected by the
-        // exact double tests (np_interp_fast's own loops), then carried to
-        // i0 + 1 .. i0 + 3 (factor >= 2: at most one segment step each)
-        const double c = 0.5 * ((double)factor - 1.0);
-        auto xp = [&](uint32_t j) { return (double)(j * factor) + c; };
-        const uint32_t last = n_lo - 1;
-        const float est = ((float)(2u * i0 + 1u) - (float)factor) / (float)(2u * factor);
-        uint32_t j = est > 0.0f ? min((uint32_t)est, last) : 0u;
-        float rr[4];
+    double sum = 0.0, sq = 0.0;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const double xv = (double)(i0 + t);
-            double y;
-            if (xv < c) {
-                y = (double)fp[0];
-            } else if (xv > xp(last)) {
-                y = (double)fp[last];
+    for (uint32_t g = 0; g < kDeredGroups; ++g) {
+        const uint32_t i0 = 4u * (blockIdx.x * 256u * kDeredGroups + g * 256u + threadIdx.x);
+        if (i0 < n) {
+            if (i0 + 4 <= n) {
+                const float4 v = *reinterpret_cast<const float4*>(x + i0);
+                // the segment of sample i0 from a float estimate corrected by the
+                // exact double tests (np_interp_fast's own loops), then carried to
+                // i0 + 1 .. i0 + 3 (factor >= 2: at most one segment step each)
+                const double c = 0.5 * ((double)factor - 1.0);
+                auto xp = [&](uint32_t j) { return (double)(j * factor) + c; };
+                const uint32_t last = n_lo - 1;
+                const float est = ((float)(2u * i0 + 1u) - (float)factor) / (float)(2u * factor);
+                uint32_t j = est > 0.0f ? min((uint32_t)est, last) : 0u;
+                float rr[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const double xv = (double)(i0 + t);
+                    double y;
+                    if (xv < c) {
+                        y = (double)fp[0];
+                    } else if (xv > xp(last)) {
+                        y = (double)fp[last];
+                    } else {
+                        while (j > 0 && xp(j) > xv) --j;
+                        while (j < last && xp(j + 1) <= xv) ++j;
+                        y = (j == last || xp(j) == xv) ? (double)fp[j]
+                                                       : __dadd_rn(__dmul_rn(slope[j], __dsub_rn(xv, xp(j))), (double)fp[j]);
+                    }
+                    const float xs = t == 0 ? v.x : t == 1 ? v.y : t == 2 ? v.z : v.w;
+                    rr[t] = (float)__dsub_rn((double)xs, y);
+                    if (STATS) {
+                        const double e = (double)rr[t];
+                        sum += e;
+                        sq += e * e;
+                    }
+                }
+                *reinterpret_cast<float4*>(out + i0) = make_float4(rr[0], rr[1], rr[2], rr[3]);
             } else {
-                while (j > 0 && xp(j) > xv) --j;
-                while (j < last && xp(j + 1) <= xv) ++j;
-                y = (j == last || xp(j) == xv) ? (double)fp[j]
-                                               : __dadd_rn(__dmul_rn(slope[j], __dsub_rn(xv, xp(j))), (double)fp[j]);
+                for (uint32_t i = i0; i < n; ++i) {
+                    const float r = (float)__dsub_rn((double)x[i], np_interp_fast(i, fp, slope, n_lo, factor));
+                    out[i] = r;
+                    if (STATS) {
+                        sum += (double)r;
+                        sq += (double)r * (double)r;
+                    }
+                }
             }
-            const float xs = t == 0 ? v.x : t == 1 ? v.y : t == 2 ? v.z : v.w;
-            rr[t] = (float)__dsub_rn((double)xs, y);
         }
-        *reinterpret_cast<float4*>(out + i0) = make_float4(rr[0], rr[1], rr[2], rr[3]);
-    } else {
-        for (uint32_t i = i0; i < n; ++i) out[i] = (float)__dsub_rn((double)x[i], np_interp_fast(i, fp, slope, n_lo, factor));
+    }
+    if (STATS) {
+        __shared__ double sh[8];
+        for (int o = 32; o > 0; o >>= 1) {
+            sum += __shfl_xor(sum, o, 64);
+            sq += __shfl_xor(sq, o, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            sh[threadIdx.x >> 6] = sum;
+            sh[4 + (threadIdx.x >> 6)] = sq;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double* p = partials + 2 * ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x);
+            p[0] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+            p[1] = (sh[4] + sh[5]) + (sh[6] + sh[7]);
+        }
+    }
+}
+
+// mean = sum / n and var = sumsq / n - mean^2 of one trial (blockIdx.x) from
+// deredden_slope_kernel<true>'s per-block partials, into stats[2b], [2b + 1]
+// as norm_finalize_kernel leaves them.  The dereddened series has mean ~0
+// (the running median is subtracted), so the one-pass variance loses nothing
+// to cancellation at float64 precision.
+__global__ __launch_bounds__(256) void norm_stats_finalize_kernel(const double* __restrict__ partials, uint32_t nblocks,
+                                                                  uint64_t n, double* __restrict__ stats)
+{
+    __shared__ double sh[8];
+    double s = 0.0, q = 0.0;
+    const double* p = partials + 2 * (uint64_t)blockIdx.x * nblocks;
+    for (uint32_t i = threadIdx.x; i < nblocks; i += 256) {
+        s += p[2 * i];
+        q += p[2 * i + 1];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        s += __shfl_xor(s, o, 64);
+        q += __shfl_xor(q, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        sh[threadIdx.x >> 6] = s;
+        sh[4 + (threadIdx.x >> 6)] = q;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double mean = ((sh[0] + sh[1]) + (sh[2] + sh[3])) / (double)n;
+        const double msq = ((sh[4] + sh[5]) + (sh[6] + sh[7])) / (double)n;
+        stats[2 * blockIdx.x] = mean;
+        stats[2 * blockIdx.x + 1] = fmax(msq - mean * mean, 0.0);
     }
 }
 
@@ -533,11 +663,11 @@ hipError_t launch_deredden_subtract(const float* x, uint64_t n, const float* rme
         hipLaunchKernelGGL(interp_slope_kernel, dim3((uint32_t)((n_lo + 255) / 256), batch), dim3(256), 0, s, rmed_lo,
                            n_lo, factor, slopes, lo_stride);
         const bool vec = ((uintptr_t)x % 16) == 0 && ((uintptr_t)out % 16) == 0 && x_stride % 4 == 0 &&
-                         out_stride % 4 == 0;
+                         out_stride % 4 == 0 && n < (1ull << 30);
         if (vec)
-            hipLaunchKernelGGL(deredden_slope_kernel, dim3((uint32_t)((n + 1023) / 1024), batch), dim3(256), 0, s, x,
-                               (uint32_t)n, rmed_lo, (const double*)slopes, (uint32_t)n_lo, factor, out, x_stride,
-                               lo_stride, out_stride);
+            hipLaunchKernelGGL(deredden_slope_kernel<false>, dim3((uint32_t)dered_norm_blocks(n), batch), dim3(256), 0,
+                               s, x, (uint32_t)n, rmed_lo, (const double*)slopes, (uint32_t)n_lo, factor, out, x_stride,
+                               lo_stride, out_stride, nullptr);
         else
             hipLaunchKernelGGL(deredden_slope1_kernel, dim3((uint32_t)((n + 255) / 256), batch), dim3(256), 0, s, x,
                                (uint32_t)n, rmed_lo, (const double*)slopes, (uint32_t)n_lo, factor, out, x_stride,
@@ -722,6 +852,31 @@ hipError_t launch_normalise(const float* x, uint64_t n, float* out, double* d_pa
     else
         hipLaunchKernelGGL(norm_apply_kernel, dim3((uint32_t)((n + 255) / 256), batch), dim3(256), 0, s, x, n, stats,
                            out, x_stride, out_stride);
+    return hipGetLastError();
+}
+
+bool dered_norm_fusable(const float* x, uint64_t n, uint64_t n_lo, uint32_t factor, const float* out,
+                        uint64_t x_stride, uint64_t out_stride)
+{
+    return factor > 1 && n_lo > 1 && n < (1ull << 30) && ((uintptr_t)x % 16) == 0 && ((uintptr_t)out % 16) == 0 &&
+           x_stride % 4 == 0 && out_stride % 4 == 0 && !std::getenv("RIPTIDE_AMD_INTERP_PER_SAMPLE") &&
+           !std::getenv("RIPTIDE_AMD_NORM_UNFUSED");
+}
+
+hipError_t launch_deredden_normalise(const float* x, uint64_t n, const float* rmed_lo, uint64_t n_lo,
+                                     uint32_t factor, float* out, uint64_t x_stride, uint64_t lo_stride,
+                                     uint64_t out_stride, uint32_t batch, hipStream_t s, double* slopes,
+                                     double* partials, double* stats)
+{
+    if (!n || !batch) return hipSuccess;
+    const uint32_t nb = (uint32_t)dered_norm_blocks(n);
+    hipLaunchKernelGGL(interp_slope_kernel, dim3((uint32_t)((n_lo + 255) / 256), batch), dim3(256), 0, s, rmed_lo,
+                       n_lo, factor, slopes, lo_stride);
+    hipLaunchKernelGGL(deredden_slope_kernel<true>, dim3(nb, batch), dim3(256), 0, s, x, (uint32_t)n, rmed_lo,
+                       (const double*)slopes, (uint32_t)n_lo, factor, out, x_stride, lo_stride, out_stride, partials);
+    hipLaunchKernelGGL(norm_stats_finalize_kernel, dim3(batch), dim3(256), 0, s, (const double*)partials, nb, n, stats);
+    hipLaunchKernelGGL(norm_apply4_kernel, dim3((uint32_t)((n + 1023) / 1024), batch), dim3(256), 0, s, out, n,
+                       (const double*)stats, out, out_stride, out_stride);
     return hipGetLastError();
 }
 

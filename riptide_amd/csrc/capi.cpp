@@ -809,7 +809,10 @@ DeredGeom dered_geom(size_t size, size_t ws, size_t minpts, size_t batch, bool d
         if (!(g.rmed_w < g.n_lo)) throw std::invalid_argument("width must be < size");
         g.rmed_floats = align_up(g.n_lo * batch, 64);
     }
-    g.partial_doubles = (size_t)kNormBlocks * batch + 2 * batch + 8;
+    // the unfused normalisation's partials, or the fused one's (two per
+    // dereddening block: launch_deredden_normalise), then 2 * batch stats
+    g.partial_doubles = std::max<size_t>((size_t)kNormBlocks, deredden ? 2 * dered_norm_blocks(size) : 0) * batch +
+                        2 * batch + 8;
     return g;
 }
 
@@ -827,6 +830,8 @@ void run_deredden_normalise(const float* d_in, size_t size, size_t batch, size_t
     double* partials = slopes + g.slope_doubles;
     const float* cur = d_in;
     size_t cur_stride = in_stride;
+    const bool fused = deredden && normalise && g.sf > 1 &&
+                       dered_norm_fusable(d_in, size, g.n_lo, (uint32_t)g.sf, d_out, in_stride, out_stride);
     if (deredden) {
         const float* rin = d_in;
         size_t rstride = in_stride;
@@ -837,6 +842,13 @@ void run_deredden_normalise(const float* d_in, size_t size, size_t batch, size_t
         }
         ck(launch_running_median(rin, g.n_lo, (uint32_t)g.rmed_w, rmed, rstride, g.n_lo, (uint32_t)batch, s),
            "running_median");
+        if (fused) {
+            const size_t np = 2 * dered_norm_blocks(size) * batch;
+            ck(launch_deredden_normalise(d_in, size, rmed, g.n_lo, (uint32_t)g.sf, d_out, in_stride, g.n_lo,
+                                         out_stride, (uint32_t)batch, s, slopes, partials, partials + np),
+               "deredden_normalise");
+            return;
+        }
         ck(launch_deredden_subtract(d_in, size, rmed, g.n_lo, (uint32_t)g.sf, d_out, in_stride, g.n_lo, out_stride,
                                     (uint32_t)batch, s, g.slope_doubles ? slopes : nullptr),
            "deredden_subtract");

@@ -72,6 +72,17 @@ hipError_t launch_scrunch(const float* x, uint64_t n_out, uint32_t factor, float
 hipError_t launch_deredden_subtract(const float* x, uint64_t n, const float* rmed_lo, uint64_t n_lo,
                                     uint32_t factor, float* out, uint64_t x_stride, uint64_t lo_stride,
                                     uint64_t out_stride, uint32_t batch, hipStream_t s, double* slopes = nullptr);
+// dereddening + normalisation with the normalisation's statistics summed by
+// the dereddening kernel (no read pass of their own).  Applies when
+// dered_norm_fusable(); partials: batch * 2 * dered_norm_blocks(n) doubles,
+// stats: 2 * batch doubles.
+inline uint64_t dered_norm_blocks(uint64_t n) { return (n + 4095) / 4096; }   // 4096 samples per block
+bool dered_norm_fusable(const float* x, uint64_t n, uint64_t n_lo, uint32_t factor, const float* out,
+                        uint64_t x_stride, uint64_t out_stride);
+hipError_t launch_deredden_normalise(const float* x, uint64_t n, const float* rmed_lo, uint64_t n_lo,
+                                     uint32_t factor, float* out, uint64_t x_stride, uint64_t lo_stride,
+                                     uint64_t out_stride, uint32_t batch, hipStream_t s, double* slopes,
+                                     double* partials, double* stats);
 hipError_t launch_interp(uint64_t n, const float* rmed_lo, uint64_t n_lo, uint32_t factor, double* out,
                          hipStream_t s);
 hipError_t launch_normalise(const float* x, uint64_t n, float* out, double* d_partials, uint32_t nblocks,

@@ -388,14 +388,15 @@ def test_segmented_snr_matches_window_path(oracle, monkeypatch, widths, bins):
 
 def test_fused_ladder_matches_per_rung(monkeypatch):
     """The fused downsampling ladder (one read of the series for every rung)
-    produces exactly the per-rung kernel's leaves, hence identical S/N."""
+    produces exactly the per-rung kernel's leaves, hence identical S/N (odd batch:
+    the two-trial blocks' last block holds one trial)."""
     import torch
     from riptide_amd import engine
     cases = [inputs.PGRAM_CASES[1], dict(n=1 << 22, tsamp=256e-6, pmin=0.1, pmax=10.0, bmin=240, bmax=260,
                                          ducy_max=0.05),
              inputs.LADDER_EDGE_CASE]        # largest rung at the fused kernel's margin (ADVICE r4)
     for case in cases:
-        x = torch.from_numpy(np.random.RandomState(7).normal(size=(2, case["n"])).astype(np.float32)).cuda()
+        x = torch.from_numpy(np.random.RandomState(7).normal(size=(3, case["n"])).astype(np.float32)).cuda()
         outs = []
         for per_rung in (False, True):
             if per_rung:

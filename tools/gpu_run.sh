@@ -18,6 +18,10 @@
 #   bash tools/gpu_run.sh TAG pmcflags CFG FLAGS...  instruction counters per RIPTIDE_AMD_CONE_FLAGS value
 #                                                    (diagnostic bits: phase attribution of VALU / SALU / LDS)
 #   bash tools/gpu_run.sh TAG attrib [CFG]           phase attribution (fill / merge / S/N / skeleton alone)
+#   bash tools/gpu_run.sh TAG ladder LIB...          ladder alone (tools/ladder_bench.py, cfg2) per library, alternated twice,
+#                                                    then the two SQ counter groups of the ladder kernel (first library)
+#   bash tools/gpu_run.sh TAG prep [ENV=V...]       dereddening + normalisation alone (tools/prep_bench.py) under
+#                                                    rocprofv3 --kernel-trace --stats, once per environment setting
 #   bash tools/gpu_run.sh TAG round                  round-end pass: attribution (cfg2), pmc (cfg2, cfg3, cfg4),
 #                                                    tests, smoke, bench cfg2 / cfg3 / cfg5, configs, prof
 set -o pipefail
@@ -203,6 +207,43 @@ PY
   done
 }
 
+do_ladder() {  # LIB...
+  for rep in 1 2; do
+    for lib in "$@"; do
+      RIPTIDE_AMD_LIB=$lib timeout -k 10 200 python -u tools/ladder_bench.py cfg2 16 10 2>&1 | grep '"round": 1' \
+        | tee -a "$O/ladder.log" || { echo "ladder $lib failed"; exit 1; }
+    done
+  done
+  local i=0
+  for grp in "${PMC_GROUPS[@]:0:2}"; do
+    i=$((i+1))
+    (cd /tmp && export TMPDIR=/tmp && export RIPTIDE_AMD_LIB=$R/$1 && timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace -f csv \
+       -d "$O/pmc_ladder/p$i" -o run -- python3 "$R/tools/ladder_bench.py" cfg2 16 2 > "$O/pmc_ladder_p$i.log" 2>&1) \
+      || fail "ladder pmc $i" "$O/pmc_ladder_p$i.log"
+  done
+  python3 tools/pmc_to_json.py "$O/pmc_ladder" "$O/pmc_ladder.json" 96 --config cfg2 --kernel downsample_fused \
+    > "$O/pmc_ladder_json.log" 2>&1 || fail pmc_ladder_json "$O/pmc_ladder_json.log"
+  head -c 600 "$O/pmc_ladder_json.log"
+}
+
+do_prep() {    # ENV=V... ("-" = none)
+  local settings=("$@"); [ ${#settings[@]} -gt 0 ] || settings=(-)
+  local i=0
+  for e in "${settings[@]}"; do
+    i=$((i+1))
+    local envs=(); [ "$e" = - ] || envs=("$e")
+    (cd /tmp && export TMPDIR=/tmp && { [ ${#envs[@]} -eq 0 ] || export "${envs[@]}"; } && timeout -k 10 200 rocprofv3 --kernel-trace --stats \
+       -d "$O/prep$i" -o run -f csv -- python3 "$R/tools/prep_bench.py" > "$O/prep$i.log" 2>&1) || fail "prep $e" "$O/prep$i.log"
+    echo "== $e $(grep ms_per_run "$O/prep$i.log")"
+    python3 - "$O/prep$i" <<'PY'
+import csv, glob, sys
+for f in glob.glob(sys.argv[1] + "/**/*kernel_stats.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        print("  %-48s calls %5s avg_us %10.2f" % (r["Name"][:48], r["Calls"], float(r["AverageNs"]) / 1e3))
+PY
+  done
+}
+
 case "$CMD" in
   tests) do_tests ;;
   bench) do_bench bench "$@" ;;
@@ -219,6 +260,8 @@ case "$CMD" in
   pmcflags) do_pmcflags "$@" ;;
   pmclib) do_pmclib "$@" ;;
   attrib) do_attrib "$@" ;;
+  ladder) do_ladder "$@" ;;
+  prep) do_prep "$@" ;;
   round)
     RIPTIDE_AMD_SCRATCH_MFLOATS=1024 RIPTIDE_AMD_COSCHED=1 do_attrib cfg2
     do_pmc cfg2

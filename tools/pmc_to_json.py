@@ -4,7 +4,7 @@ the cone kernel from FETCH_SIZE / WRITE_SIZE (rocprofv3, KB units), with the
 gfx950 correction of MI355X_MICROARCH.md (FETCH_SIZE reports half the bytes of
 wide streaming reads: x2), plus the SQ counters as ratios.
 
-usage: tools/pmc_to_json.py gpurun_out/<pmc dir> profiles/<name>.json TRIALS [--config CFG]
+usage: tools/pmc_to_json.py gpurun_out/<pmc dir> profiles/<name>.json TRIALS [--config CFG] [--kernel NAME]
 (TRIALS = trials the profiled run processed: tools/gpu_run.sh pmc cfg2 runs
 bench.py warmup 1 + steps 1 at batch 2 -> 4; pmc CFG runs tools/ab_flags.py,
 2 rounds x 4 runs x 8 trials -> 64)
@@ -21,12 +21,13 @@ from collections import defaultdict
 def main():
     root, out, trials = sys.argv[1], sys.argv[2], int(sys.argv[3])
     config = sys.argv[sys.argv.index("--config") + 1] if "--config" in sys.argv else "cfg2"
+    kernel = sys.argv[sys.argv.index("--kernel") + 1] if "--kernel" in sys.argv else "cone_kernel"
     sums = defaultdict(float)
     disp = defaultdict(set)
     for f in sorted(glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True)):
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                if "cone_kernel" not in r.get("Kernel_Name", ""):
+                if kernel not in r.get("Kernel_Name", ""):
                     continue
                 sums[r["Counter_Name"]] += float(r["Counter_Value"])
                 disp[r["Counter_Name"]].add((f, r.get("Dispatch_Id")))
@@ -37,7 +38,7 @@ def main():
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from bench import source_digest
     res = {
-        "kernel": "cone_kernel",
+        "kernel": kernel,
         "config": config,
         "source": root,
         "commit": commit,
