@@ -142,17 +142,9 @@ __global__ __launch_bounds__(kRmedTile) void rmed_small_kernel(const float* __re
     out[i] = res;
 }
 
-// Small windows, kRmedRun consecutive outputs per thread: the first by the
-// counting search of rmed_small_kernel, each next one from the previous
-// median m (one sample leaves the window, one enters, so the median moves by
-// at most one place in sorted order): m itself if its rank still fits, else
-// the largest window value below m or the smallest above it, each verified
-// by its rank; any miss (NaN data) takes the full search.  The value returned
-// is then the window's first element equal to the median (the element the
-// full search returns: the median value is unique, and of equal values it
-// picks the first in window order -- +0.0 / -0.0 included).  kRmedRun is
-// odd, so the 64 lanes' LDS reads (stride kRmedRun) land on distinct banks.
-constexpr int kRmedRun = 7;
+// outputs per thread of rmed_run_kernel (odd: the 64 lanes' LDS reads at
+// stride kRmedRun land on distinct banks)
+constexpr int kRmedRun = 3;   // 3 / 5 / 7 / 9: 197 / 202 / 234 / 264 us (profiles/r05p7_prep_rmed_run.log)
 
 __device__ __forceinline__ void rank_of(const float* win, int width, float v, int& less, int& leq)
 {
@@ -176,54 +168,112 @@ __device__ __forceinline__ void rank_of(const float* win, int width, float v, in
     leq = (q0 + q1) + (q2 + q3);
 }
 
+// One pass over the window: the rank of v (values < v, values <= v) and its
+// neighbours in sorted order (the largest value below v, the smallest above).
+__device__ __forceinline__ void rank_nb(const float* win, int width, float v, int& less, int& leq, float& below,
+                                        float& above)
+{
+    int l0 = 0, l1 = 0, q0 = 0, q1 = 0;
+    float b0 = -INFINITY, b1 = -INFINITY, a0 = INFINITY, a1 = INFINITY;
+    int k = 0;
+    for (; k + 2 <= width; k += 2) {
+        const float u0 = win[k], u1 = win[k + 1];
+        l0 += u0 < v; q0 += u0 <= v;
+        l1 += u1 < v; q1 += u1 <= v;
+        b0 = (u0 < v && u0 > b0) ? u0 : b0;
+        b1 = (u1 < v && u1 > b1) ? u1 : b1;
+        a0 = (u0 > v && u0 < a0) ? u0 : a0;
+        a1 = (u1 > v && u1 < a1) ? u1 : a1;
+    }
+    if (k < width) {
+        const float u = win[k];
+        l0 += u < v; q0 += u <= v;
+        b0 = (u < v && u > b0) ? u : b0;
+        a0 = (u > v && u < a0) ? u : a0;
+    }
+    less = l0 + l1;
+    leq = q0 + q1;
+    below = b0 > b1 ? b0 : b1;
+    above = a0 < a1 ? a0 : a1;
+}
+
+// Small windows, kRmedRun consecutive outputs per thread, each found by a
+// walk in sorted order from a starting value m: one pass gives m's rank and
+// its two neighbours; m is the median when its rank interval holds w/2,
+// else the walk moves to the neighbour on the median's side.  The first
+// output starts from the window value closest to the window's mean (for
+// noise-like data a few places from the median; the previous round's full
+// counting search tried ~w/2 candidates at w reads each), each next one from
+// the previous median (one sample leaves, one enters: at most one step).  A
+// walk longer than kRmedMaxSteps or one that runs off the window's values
+// (NaN / infinite data) takes the full counting search.  The value returned
+// is the window's first element equal to the median (the element the full
+// search returns: the median value is unique, and of equal values it picks
+// the first in window order -- +0.0 / -0.0 included).  kRmedRun is odd, so
+// the 64 lanes' LDS reads (stride kRmedRun) land on distinct banks.
+constexpr int kRmedMaxSteps = 48;
+
+template <int RUN>
 __global__ __launch_bounds__(kRmedTile) void rmed_run_kernel(const float* __restrict__ x, uint64_t n, int width,
                                                              float* __restrict__ out, uint64_t x_stride,
                                                              uint64_t out_stride)
 {
-    __shared__ float span[kRmedTile * kRmedRun + kRmedSmallMax];
+    __shared__ float span[kRmedTile * RUN + kRmedSmallMax];
     x += (uint64_t)blockIdx.y * x_stride;
     out += (uint64_t)blockIdx.y * out_stride;
     const int half = width / 2;
-    const int64_t i0 = (int64_t)blockIdx.x * (kRmedTile * kRmedRun);
-    for (int k = threadIdx.x; k < kRmedTile * kRmedRun + width - 1; k += kRmedTile) {
+    const int64_t i0 = (int64_t)blockIdx.x * (kRmedTile * RUN);
+    for (int k = threadIdx.x; k < kRmedTile * RUN + width - 1; k += kRmedTile) {
         int64_t idx = i0 - half + k;
         idx = idx < 0 ? 0 : (idx >= (int64_t)n ? (int64_t)n - 1 : idx);
         span[k] = x[idx];
     }
     __syncthreads();
-    const int64_t ib = i0 + (int64_t)threadIdx.x * kRmedRun;
+    const int64_t ib = i0 + (int64_t)threadIdx.x * RUN;
     float m = 0.0f;
     bool have = false;
-    for (int r = 0; r < kRmedRun; ++r) {
+    for (int r = 0; r < RUN; ++r) {
         if (ib + r >= (int64_t)n) return;
-        const float* win = span + threadIdx.x * kRmedRun + r;
+        const float* win = span + threadIdx.x * RUN + r;
+        if (!have) {
+            // the window value closest to the window's mean
+            float s0 = 0.0f, s1 = 0.0f;
+            int k = 0;
+            for (; k + 2 <= width; k += 2) {
+                s0 += win[k];
+                s1 += win[k + 1];
+            }
+            if (k < width) s0 += win[k];
+            const float mean = (s0 + s1) / (float)width;
+            m = win[half];
+            float bd = fabsf(m - mean);
+            for (k = 0; k < width; ++k) {
+                const float d = fabsf(win[k] - mean);
+                if (d < bd) {
+                    bd = d;
+                    m = win[k];
+                }
+            }
+        }
         bool found = false;
-        if (have) {
+        for (int step = 0; step < kRmedMaxSteps; ++step) {
             int less, leq;
-            rank_of(win, width, m, less, leq);
+            float below, above;
+            rank_nb(win, width, m, less, leq, below, above);
             if (less <= half && half < leq) {
                 found = true;
-            } else if (less > half || leq <= half) {
-                // the neighbour in sorted order: max below m or min above it
-                const bool down = less > half;
-                float c = down ? -INFINITY : INFINITY;
-                for (int k = 0; k < width; ++k) {
-                    const float u = win[k];
-                    c = down ? (u < m && u > c ? u : c) : (u > m && u < c ? u : c);
-                }
-                rank_of(win, width, c, less, leq);
-                if (less <= half && half < leq) {
-                    m = c;
-                    found = true;
-                }
+                break;
             }
-            if (found) {
-                // the window's first element equal to the median
-                int k = 0;
-                while (k < width && !(win[k] == m)) ++k;
-                if (k < width) m = win[k];
-                else found = false;
-            }
+            const float c = less > half ? below : above;
+            if (!(c > -INFINITY && c < INFINITY)) break;
+            m = c;
+        }
+        if (found) {
+            // the window's first element equal to the median
+            int k = 0;
+            while (k < width && !(win[k] == m)) ++k;
+            if (k < width) m = win[k];
+            else found = false;
         }
         if (!found) {
             // the full counting search (rmed_small_kernel)
@@ -296,9 +346,19 @@ hipError_t launch_running_median(const float* x, uint64_t n, uint32_t width, flo
         hipLaunchKernelGGL(rmed_small_kernel, dim3((uint32_t)((n + kRmedTile - 1) / kRmedTile), batch),
                            dim3(kRmedTile), 0, s, x, n, (int)width, out, x_stride, out_stride);
     } else if (width <= (uint32_t)kRmedSmallMax) {
-        const uint64_t per = (uint64_t)kRmedTile * kRmedRun;
-        hipLaunchKernelGGL(rmed_run_kernel, dim3((uint32_t)((n + per - 1) / per), batch), dim3(kRmedTile), 0, s, x, n,
-                           (int)width, out, x_stride, out_stride);
+        static const int run = [] {
+            const char* e = std::getenv("RIPTIDE_AMD_RMED_RUN");
+            return e ? std::atoi(e) : kRmedRun;
+        }();
+        auto go = [&](auto kern, int r) {
+            const uint64_t per = (uint64_t)kRmedTile * r;
+            hipLaunchKernelGGL(kern, dim3((uint32_t)((n + per - 1) / per), batch), dim3(kRmedTile), 0, s, x, n,
+                               (int)width, out, x_stride, out_stride);
+        };
+        if (run == 5) go(rmed_run_kernel<5>, 5);
+        else if (run == 7) go(rmed_run_kernel<7>, 7);
+        else if (run == 9) go(rmed_run_kernel<9>, 9);
+        else go(rmed_run_kernel<kRmedRun>, kRmedRun);
     } else {
         hipLaunchKernelGGL(rmed_large_kernel, dim3((uint32_t)n, batch), dim3(256), 0, s, x, n, (int)width,
                            out, x_stride, out_stride);
@@ -527,30 +587,46 @@ __global__ __launch_bounds__(256) void deredden_slope_kernel(const float* __rest
     for (uint32_t g = 0; g < kDeredGroups; ++g) {
         const uint32_t i0 = 4u * (blockIdx.x * 256u * kDeredGroups + g * 256u + threadIdx.x);
         if (i0 < n) {
-            if (i0 + 4 <= n) {
+            if (i0 + 4 <= n && factor >= 4) {
                 const float4 v = *reinterpret_cast<const float4*>(x + i0);
-                // the segment of sample i0 from a float estimate corrected by the
-                // exact double tests (np_interp_fast's own loops), then carried to
-                // i0 + 1 .. i0 + 3 (factor >= 2: at most one segment step each)
-                const double c = 0.5 * ((double)factor - 1.0);
-                auto xp = [&](uint32_t j) { return (double)(j * factor) + c; };
+                // the segment j of sample i0 from a float estimate corrected
+                // by np_interp_fast's exact tests, on xj = xp[j] carried by
+                // adding / subtracting factor (exact: integers and
+                // half-integers below 2^31); factor >= 4, so i0 .. i0 + 3 lie
+                // in segment j or j + 1, whose fp / slope loads go out once,
+                // ahead of the four samples
+                const double c = 0.5 * ((double)factor - 1.0), df = (double)factor;
                 const uint32_t last = n_lo - 1;
+                const double xlast = (double)(last * factor) + c;
+                const double x0 = (double)i0;
                 const float est = ((float)(2u * i0 + 1u) - (float)factor) / (float)(2u * factor);
                 uint32_t j = est > 0.0f ? min((uint32_t)est, last) : 0u;
+                double xj = (double)(j * factor) + c;
+                while (j > 0 && xj > x0) {
+                    --j;
+                    xj -= df;
+                }
+                while (j < last && xj + df <= x0) {
+                    ++j;
+                    xj += df;
+                }
+                const uint32_t j1 = min(j + 1, last);
+                const double fa = (double)fp[j], fb = (double)fp[j1];
+                const double sa = slope[min(j, last - 1)], sb = slope[min(j1, last - 1)];
                 float rr[4];
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
-                    const double xv = (double)(i0 + t);
+                    const double xv = x0 + (double)t;
                     double y;
                     if (xv < c) {
                         y = (double)fp[0];
-                    } else if (xv > xp(last)) {
+                    } else if (xv > xlast) {
                         y = (double)fp[last];
                     } else {
-                        while (j > 0 && xp(j) > xv) --j;
-                        while (j < last && xp(j + 1) <= xv) ++j;
-                        y = (j == last || xp(j) == xv) ? (double)fp[j]
-                                                       : __dadd_rn(__dmul_rn(slope[j], __dsub_rn(xv, xp(j))), (double)fp[j]);
+                        const bool nx = j < last && xj + df <= xv;
+                        const uint32_t jj = nx ? j1 : j;
+                        const double xp = nx ? xj + df : xj, fv = nx ? fb : fa, sl = nx ? sb : sa;
+                        y = (jj == last || xp == xv) ? fv : __dadd_rn(__dmul_rn(sl, __dsub_rn(xv, xp)), fv);
                     }
                     const float xs = t == 0 ? v.x : t == 1 ? v.y : t == 2 ? v.z : v.w;
                     rr[t] = (float)__dsub_rn((double)xs, y);
@@ -562,7 +638,7 @@ __global__ __launch_bounds__(256) void deredden_slope_kernel(const float* __rest
                 }
                 *reinterpret_cast<float4*>(out + i0) = make_float4(rr[0], rr[1], rr[2], rr[3]);
             } else {
-                for (uint32_t i = i0; i < n; ++i) {
+                for (uint32_t i = i0; i < min(i0 + 4, n); ++i) {
                     const float r = (float)__dsub_rn((double)x[i], np_interp_fast(i, fp, slope, n_lo, factor));
                     out[i] = r;
                     if (STATS) {

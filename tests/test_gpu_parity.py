@@ -165,6 +165,72 @@ def test_running_median_reference_cases(rt):
         assert np.array_equal(rt.running_median(x64, w), rt.fast_running_median(x64, w, min_points=39))
 
 
+def test_running_median_walk_matches_counting(rt, monkeypatch):
+    """The run kernel's walk in sorted order (rmed_run_kernel) returns the
+    same element as the full counting search (rmed_small_kernel,
+    RIPTIDE_AMD_RMED_COUNTING=1), bit for bit (the sign of zero included), on
+    data that defeats its near-median start or its walk: heavy duplicates,
+    +0.0 / -0.0 mixes, monotone runs, step changes, outliers, infinities and
+    NaNs."""
+    rs = np.random.RandomState(11)
+    n = 5003
+    cases = [np.round(rs.normal(size=n) * 2.0) / 2.0,                        # few distinct values
+             np.where(rs.rand(n) < 0.5, 0.0, -0.0) + np.where(rs.rand(n) < 0.1, rs.normal(size=n), 0.0),
+             np.arange(n, dtype=np.float64), np.arange(n, 0, -1, dtype=np.float64),
+             np.where(np.arange(n) % 400 < 200, 100.0, -100.0) + rs.normal(size=n),
+             rs.standard_cauchy(size=n),
+             np.where(rs.rand(n) < 0.02, np.inf, rs.normal(size=n)),
+             np.where(rs.rand(n) < 0.02, -np.inf, rs.normal(size=n)),
+             np.where(rs.rand(n) < 0.05, np.nan, rs.normal(size=n))]
+    for w in (3, 37, 101, 255):
+        for x in cases:
+            x = x.astype(np.float32)
+            monkeypatch.setenv("RIPTIDE_AMD_RMED_COUNTING", "1")
+            ref = rt.running_median(x, w)
+            monkeypatch.delenv("RIPTIDE_AMD_RMED_COUNTING")
+            got = rt.running_median(x, w)
+            assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), w
+
+
+@pytest.mark.parametrize("ws", [203, 303, 404, 1001, 15625])
+def test_deredden_normalise_batch_vs_oracle(rt, oracle, monkeypatch, ws):
+    """Device dereddening of a batch (scrunch factors 2, 3, 4, 9, 154: the
+    two-segment fast interpolation needs factor >= 4, the others take the
+    per-sample form) bit-identical to the oracle's fast_running_median
+    subtraction, and the normalisation -- statistics summed by the
+    dereddening kernel, or by their own read passes with
+    RIPTIDE_AMD_NORM_UNFUSED -- within 2e-6 of the oracle's numpy
+    mean / var.  Rows of 30011 samples in 16-byte aligned rows of 30016
+    floats: the 16-byte path with a ragged last group."""
+    import torch
+    from riptide_amd import engine
+    n, B, mp = 30011, 3, 101
+    rs = np.random.RandomState(ws)
+    xs = (rs.normal(size=(B, n)) + 5.0 + np.sin(np.arange(n) / 700.0)).astype(np.float32)
+    big = torch.zeros((B, 30016), dtype=torch.float32, device="cuda")
+    big[:, :n] = torch.from_numpy(xs).cuda()
+    x = big[:, :n]
+    dered = engine.deredden_normalise(x, ws, mp, normalise=False).cpu().numpy()        # one-sample form
+    ob = torch.zeros((B, 30016), dtype=torch.float32, device="cuda")
+    engine.deredden_normalise(x, ws, mp, normalise=False, out=ob[:, :n])
+    dered4 = ob[:, :n].cpu().numpy()                                                       # 16-byte form
+    outs = {}
+    for unfused in (False, True):
+        if unfused:
+            monkeypatch.setenv("RIPTIDE_AMD_NORM_UNFUSED", "1")
+        else:
+            monkeypatch.delenv("RIPTIDE_AMD_NORM_UNFUSED", raising=False)
+        ob = torch.zeros((B, 30016), dtype=torch.float32, device="cuda")
+        engine.deredden_normalise(x, ws, mp, out=ob[:, :n])
+        outs[unfused] = ob[:, :n].cpu().numpy()
+    for b in range(B):
+        ref = np.asarray(xs[b] - oracle.fast_running_median(xs[b], ws, mp), dtype=np.float32)
+        assert np.array_equal(dered[b], ref) and np.array_equal(dered4[b], ref)
+        norm = oracle.normalise(ref)
+        for unfused in (False, True):
+            assert np.allclose(outs[unfused][b], norm, rtol=2e-6, atol=2e-6)
+
+
 @pytest.mark.parametrize("ws,mp", inputs.FAST_RMED_CASES)
 def test_fast_running_median_exact(rt, golden, ws, mp):
     out = rt.fast_running_median(inputs.noise(30011, 14), ws, mp)
