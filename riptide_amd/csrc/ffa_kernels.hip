@@ -159,9 +159,16 @@ __global__ __launch_bounds__(256) void downsample_fused_kernel(
     __syncthreads();
     const double last = (double)n_in - 1.0;
     const uint32_t b0 = (uint32_t)s0;
+    // Only a block staged up to the end of the series can hold windows that
+    // min(floor(end), N - 1) clips (otherwise end < s_end + margin <= l_end
+    // < N).  Every other block has cnt >= floor(f) (floor and rounding are
+    // monotone and start + floor(f) is exact), so with CC = floor(f) + 1 its
+    // reads w[1 .. CC - 2] all add and only w[CC - 1] depends on cnt; the
+    // clipping block takes the general window sum.
+    const bool tail = l_end >= n_in;
     // one output k of a rung of factor f: window_sum or, with CC > 0 (f <
-    // CC), the window's reads w[0 .. CC) at immediate offsets, the ones past
-    // cnt - 1 adding -0.0 (an exact no-op), instead of window_sum's groups of
+    // CC), the window's reads w[0 .. CC) at immediate offsets, w[CC - 1]
+    // adding -0.0 (an exact no-op) when cnt = CC - 1, instead of window_sum's groups of
     // eight (at f ~ 1.5, most of the ladder's outputs: 8 reads, selects and
     // adds for 1-2 terms).  cnt <= floor(f) + 1: reads w[0 .. floor(f)],
     // inside the staged margin (kDsFusedMargin >= ceil(f) + 2).
@@ -171,7 +178,7 @@ __global__ __launch_bounds__(256) void downsample_fused_kernel(
         const double end = __dadd_rn(start, f);
         const double fs = floor(start);
         double dmax = floor(end);
-        if (dmax > last) dmax = last;
+        if (CC == 0 && dmax > last) dmax = last;
         const uint32_t imin = (uint32_t)fs, imax = (uint32_t)dmax;
         const float wmin = (float)__dsub_rn(__dadd_rn(fs, 1.0), start);
         const float wmax = (float)__dsub_rn(end, dmax);
@@ -184,7 +191,8 @@ __global__ __launch_bounds__(256) void downsample_fused_kernel(
             for (int j = 0; j < CC; ++j) v[j] = w[j];
             acc = __fmul_rn(wmin, v[0]);
 #pragma unroll
-            for (int j = 1; j < CC; ++j) acc = __fadd_rn(acc, (uint32_t)j < cnt ? v[j] : -0.0f);
+            for (int j = 1; j < CC - 1; ++j) acc = __fadd_rn(acc, v[j]);
+            acc = __fadd_rn(acc, (uint32_t)(CC - 1) < cnt ? v[CC - 1] : -0.0f);
         } else {
             acc = window_sum(w, wmin, cnt);
         }
@@ -203,6 +211,10 @@ __global__ __launch_bounds__(256) void downsample_fused_kernel(
         auto rung = [&](auto cc) {
             for (uint32_t k = k_lo + threadIdx.x; k < k_hi; k += 256) o[k] = output(cc, f, k);
         };
+        if (tail) {
+            rung(IntC<0>{});
+            continue;
+        }
         switch ((int)f + 1) {
         case 2: rung(IntC<2>{}); break;
         case 3: rung(IntC<3>{}); break;
