@@ -176,10 +176,13 @@ def _drop_cache(fn):
 
 def bench_cfg5(args, torch, dist, world, rank, local, dev):
     """BASELINE configs[4] (cfg5): SIGPROC .tim DM trials of 2^23 samples @ 64 us
-    searched from files to peak lists, the rffa search stage
-    (pipeline.py:177-189 with worker_pool.py:47-70) on the GPU worker pool:
+    searched from files to clustered peak lists, the rffa search and
+    clustering stages (pipeline.py:177-215 with worker_pool.py:47-70) on the
+    GPU worker pool:
     file read + H2D (8-bit files converted on the device) + deredden +
-    normalise + 3 search ranges (example.yaml) + device peak detection.
+    normalise + 3 search ranges (example.yaml) + device peak detection, then
+    the gathered peaks sorted by period and clustered in frequency
+    (cluster1d, radius 0.2 / Tobs).
     Each rank searches its round-robin share of the node's file list
     (dispatch.search_files: DMIterator chunks of --batch files, the next chunk
     read into a bounded page-locked ring while the current one is on the
@@ -190,6 +193,7 @@ def bench_cfg5(args, torch, dist, world, rank, local, dev):
     import tempfile
     sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
     import inputs
+    from riptide_amd.clustering import cluster_peaks
     from riptide_amd.dispatch import search_files
     from riptide_amd.reading import write_sigproc
     from riptide_amd.worker_pool import GpuWorkerPool
@@ -243,12 +247,15 @@ def bench_cfg5(args, torch, dist, world, rank, local, dev):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         peaks = search_files(fnames, pool, chunksize=args.batch)
+        # Pipeline.search's sort + Pipeline.cluster_peaks (pipeline.py:186,
+        # 192-215) on the gathered list, inside the timed region
+        _, clusters = cluster_peaks(peaks, CFG5_CLUSTER_RADIUS, c["n"] * c["tsamp"])
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         if world > 1:
             dist.barrier()
             elapsed = rank_max(torch, dist, elapsed, dev)
-        res[mode] = (elapsed, len(peaks))
+        res[mode] = (elapsed, len(peaks), len(clusters))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         lst = os.path.join(tmp, "files.txt")
@@ -263,7 +270,7 @@ def bench_cfg5(args, torch, dist, world, rank, local, dev):
     if rank == 0:
         cold, warm = res["cold"], res["warm"]
         line = {
-            "metric": "DM trials/sec files->peaks (cfg5 rffa search stage, 2^23 samples @ 64 us, 3 ranges)",
+            "metric": "DM trials/sec files->peak clusters (cfg5 rffa search + clustering stages, 2^23 samples @ 64 us, 3 ranges)",
             "value": total / cold[0], "unit": "DM trials/s", "n_gpus": world, "steps": 1, "warmup": 1,
             "ms_per_step": cold[0] * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32", "data": "synthetic SIGPROC files (tests/golden/inputs.py cfg5_trial k mod 64; 6 of 8 "
@@ -273,14 +280,21 @@ def bench_cfg5(args, torch, dist, world, rank, local, dev):
                                    "medium / long, smin 6), dispatch.search_files, DMIterator chunks of --batch "
                                    "files with the next chunk prefetched",
                        "files_per_gpu": files, "chunk": args.batch, "peaks_found": cold[1],
+                       "clusters_found": cold[2], "clustering_radius_per_tobs": CFG5_CLUSTER_RADIUS,
+                       "timed": "file read + H2D + deredden + normalise + 3 ranges' periodograms + device "
+                                "peak detection + gather + sort by period + cluster1d (pipeline.py:177-215)",
                        "parallelism": f"dm-trials x{world} (independent, weak scaling)" + REHEARSAL},
             "cold": {"value": total / cold[0], "seconds": cold[0]},
-            "warm": {"value": total / warm[0], "seconds": warm[0], "peaks_found": warm[1]},
+            "warm": {"value": total / warm[0], "seconds": warm[0], "peaks_found": warm[1],
+                     "clusters_found": warm[2]},
         }
         if cpu is not None:
             line["cpu_baseline"] = cpu
         print(json.dumps(line), flush=True)
 
+
+# example.yaml `clustering.radius` (units of 1 / Tobs; pipeline.py:200)
+CFG5_CLUSTER_RADIUS = 0.2
 
 CFG3 = dict(n=1 << 22, tsamp=256e-6, pmin=0.2, pmax=5.0, bmin=240, bmax=260, ducy_max=0.2,
             rmed_width=4.0, rmed_minpts=101, trials=1024)
@@ -300,13 +314,17 @@ def rank_max(torch, dist, x, dev):
     return float(t.item())
 
 
-def self_check(torch, dist, engine, plan, xbuf, snr, c, local, world, dev):
-    """After the timed region: trial 0 of the last timed batch (its
-    dereddened + normalised series is still in xbuf[0]) through a plan with
-    the library's default transform grouping (96 Mi floats per buffer: the
-    schedule every GPU parity test runs); True on every rank only if its S/N
-    is bit-identical to the benchmarked schedule's (snr[0])."""
-    saved = {k: os.environ.pop(k, None) for k in ("RIPTIDE_AMD_SCRATCH_MFLOATS", "RIPTIDE_AMD_COSCHED")}
+def self_check(torch, dist, engine, plan, xbuf, snr, c, local, world, dev, ntrials):
+    """After the timed region: EVERY trial of the last timed batch (their
+    dereddened + normalised series are still in xbuf[0:ntrials]) through a
+    plan with the library's default transform grouping (96 Mi floats per
+    buffer, the schedule every GPU parity test runs) at batch 1 -- one trial
+    per workgroup, so none of the benchmarked trial loop's later-trial paths
+    (the next trial's fill overlapping this trial's stores, the zero-row
+    rewrite) -- and True on every rank only if all ntrials S/N arrays are
+    bit-identical to the benchmarked schedule's (snr[b])."""
+    saved = {k: os.environ.pop(k, None) for k in ("RIPTIDE_AMD_SCRATCH_MFLOATS", "RIPTIDE_AMD_COSCHED",
+                                                   "RIPTIDE_AMD_TRIALS_PER_WG")}
     try:
         ref = engine.PeriodogramPlan.for_search(c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"],
                                                 ducy_max=c["ducy_max"], device=local)
@@ -314,14 +332,19 @@ def self_check(torch, dist, engine, plan, xbuf, snr, c, local, world, dev):
         for k, v in saved.items():
             if v is not None:
                 os.environ[k] = v
-    got = ref.run(xbuf[0:1].contiguous(), check=True)
-    torch.cuda.synchronize()
-    same = bool(torch.equal(got[0], snr[0]))
-    if not same:
-        bad = int((got[0] != snr[0]).sum().item())
-        print(f"bench self-check: {bad} S/N values of trial 0 differ from the default-schedule plan",
-              file=sys.stderr, flush=True)
-    del ref, got
+    bad = []
+    out = torch.empty((1, ref.length, ref.num_widths), dtype=torch.float32, device=dev)
+    ws = torch.empty(ref.workspace_bytes(1), dtype=torch.uint8, device=dev)
+    for b in range(ntrials):
+        ref.run(xbuf[b:b + 1], out=out, workspace=ws, check=True)
+        torch.cuda.synchronize()
+        if not torch.equal(out[0], snr[b]):
+            bad.append((b, int((out[0] != snr[b]).sum().item())))
+    same = not bad
+    if bad:
+        print(f"bench self-check: S/N of trials differ from their batch-1 default-schedule runs "
+              f"(trial, values): {bad}", file=sys.stderr, flush=True)
+    del ref, out, ws
     if world > 1:
         same = rank_max(torch, dist, 0.0 if same else 1.0, dev) == 0.0
     return same
@@ -408,8 +431,10 @@ def bench_cfg3(args, torch, dist, world, rank, local, dev):
         elapsed = rank_max(torch, dist, elapsed, dev)
     cone = engine.profile_read(0)
     stats = plan.stats()
-    # the last batch's first trial through the default-schedule plan
-    checked = None if args.no_self_check else self_check(torch, dist, engine, plan, xbuf, snr, c, local, world, dev)
+    # every trial of the last batch through the default-schedule plan at batch 1
+    last = len(mine) - B * ((len(mine) - 1) // B)
+    checked = None if args.no_self_check else self_check(torch, dist, engine, plan, xbuf, snr, c, local, world, dev,
+                                                         last)
     if rank == 0:
         pmc, pmc_reason = pmc_traffic("cfg3")
         rf = roofline(engine, cone, stats, B, pmc, pmc_reason)
@@ -448,6 +473,9 @@ def bench_cfg3(args, torch, dist, world, rank, local, dev):
             },
             "roofline": rf,
             "checked": checked,
+            "checked_trials": None if checked is None else last,
+            "check_basis": "every trial of the last timed batch == its batch-1 run through the default "
+                           "96 M-float schedule, bit for bit",
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baselines("cfg3")
@@ -593,7 +621,8 @@ def main():
     cone = engine.profile_read(0)
     ladder = engine.profile_read(1)
     stats = plan.stats()
-    checked = None if args.no_self_check else self_check(torch, dist, engine, plan, xbuf, snr, c, local, world, dev)
+    checked = None if args.no_self_check else self_check(torch, dist, engine, plan, xbuf, snr, c, local, world, dev,
+                                                         B)
 
     if rank == 0:
         pmc, pmc_reason = pmc_traffic()
@@ -643,6 +672,9 @@ def main():
             },
             "roofline": rf,
             "checked": checked,
+            "checked_trials": None if checked is None else B,
+            "check_basis": "every trial of the last timed batch == its batch-1 run through the default "
+                           "96 M-float schedule, bit for bit",
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baselines("cfg2")

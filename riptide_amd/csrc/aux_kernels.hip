@@ -346,10 +346,10 @@ hipError_t launch_running_median(const float* x, uint64_t n, uint32_t width, flo
         hipLaunchKernelGGL(rmed_small_kernel, dim3((uint32_t)((n + kRmedTile - 1) / kRmedTile), batch),
                            dim3(kRmedTile), 0, s, x, n, (int)width, out, x_stride, out_stride);
     } else if (width <= (uint32_t)kRmedSmallMax) {
-        static const int run = [] {
-            const char* e = std::getenv("RIPTIDE_AMD_RMED_RUN");
-            return e ? std::atoi(e) : kRmedRun;
-        }();
+        // read per launch (like RIPTIDE_AMD_RMED_COUNTING), so one process
+        // can test every run length
+        const char* e = std::getenv("RIPTIDE_AMD_RMED_RUN");
+        const int run = e ? std::atoi(e) : kRmedRun;
         auto go = [&](auto kern, int r) {
             const uint64_t per = (uint64_t)kRmedTile * r;
             hipLaunchKernelGGL(kern, dim3((uint32_t)((n + per - 1) / per), batch), dim3(kRmedTile), 0, s, x, n,
@@ -869,9 +869,11 @@ __global__ __launch_bounds__(kNormBlock) void norm_finalize_kernel(const double*
     if (threadIdx.x == 0) stats[2 * blockIdx.x + mode] = t / (double)n;
 }
 
-// four samples per thread (16-byte aligned rows; norm_apply_kernel otherwise)
-__global__ __launch_bounds__(256) void norm_apply4_kernel(const float* __restrict__ x, uint64_t n,
-                                                          const double* __restrict__ stats, float* __restrict__ out,
+// four samples per thread (16-byte aligned rows; norm_apply_kernel otherwise).
+// x and out may be the same buffer (launch_deredden_normalise applies in
+// place), so neither is __restrict__.
+__global__ __launch_bounds__(256) void norm_apply4_kernel(const float* x, uint64_t n,
+                                                          const double* __restrict__ stats, float* out,
                                                           uint64_t x_stride, uint64_t out_stride)
 {
     const uint64_t i0 = 4 * ((uint64_t)blockIdx.x * 256 + threadIdx.x);

@@ -407,6 +407,10 @@ void run_cone_launches(const DevicePlan& P, ConeArgs a, uint32_t batch, hipStrea
     a.trials_per_wg = cone_trials_per_wg();
     a.flags = kConeDefaultFeatures;
     if (const char* e = std::getenv("RIPTIDE_AMD_CONE_FLAGS")) a.flags = (uint32_t)std::strtoul(e, nullptr, 0);
+    // the 4/5-slot instances have no dense per-level path since round 5: the
+    // fused two-level merge is their only merge, so the bit cannot be turned
+    // off (an A/B value without it would leave their units unwritten)
+    a.flags |= kConeFuse2;
     a.blob = P.d_blob;
     const std::vector<Launch>& Ls = P.ex.launches;
     DeviceGuard dg(P.device);

@@ -860,6 +860,13 @@ static void validate_blob(const ConeItem& it, uint32_t p, int smax, int rw, cons
     }
     if (resolved_slots(smax)) {
         const int Q = (rw + 1) / 2;
+        // The zero row lies past the fill; a final whole unit's output level
+        // (S/N stride) or the segmented S/N's maxima / exchange areas may
+        // cover it.  That is allowed: the kernel writes it at the workgroup's
+        // start and again after every trial's S/N (behind the trial loop's
+        // barrier, ffa_kernels.hip cone_kernel), before the next trial's
+        // first merge step reads it; the next trial's DMA (below 4 * fill)
+        // never touches it.
         const uint32_t zero_row = w[kHdrZero];
         if (zero_row && (tile || (L % 2) || zero_row < 4 * fill || zero_row + 64 * (uint32_t)smax > (uint32_t)kLdsDataFloats))
             throw std::runtime_error("schedule: bad zero row");

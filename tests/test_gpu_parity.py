@@ -165,13 +165,16 @@ def test_running_median_reference_cases(rt):
         assert np.array_equal(rt.running_median(x64, w), rt.fast_running_median(x64, w, min_points=39))
 
 
-def test_running_median_walk_matches_counting(rt, monkeypatch):
-    """The run kernel's walk in sorted order (rmed_run_kernel) returns the
+@pytest.mark.parametrize("run", ["3", "5", "7", "9"])
+def test_running_median_walk_matches_counting(rt, monkeypatch, run):
+    """The run kernel's walk in sorted order (rmed_run_kernel<RUN>, every
+    instantiation: RIPTIDE_AMD_RMED_RUN is read per launch) returns the
     same element as the full counting search (rmed_small_kernel,
     RIPTIDE_AMD_RMED_COUNTING=1), bit for bit (the sign of zero included), on
     data that defeats its near-median start or its walk: heavy duplicates,
     +0.0 / -0.0 mixes, monotone runs, step changes, outliers, infinities and
     NaNs."""
+    monkeypatch.setenv("RIPTIDE_AMD_RMED_RUN", run)
     rs = np.random.RandomState(11)
     n = 5003
     cases = [np.round(rs.normal(size=n) * 2.0) / 2.0,                        # few distinct values
@@ -229,6 +232,12 @@ def test_deredden_normalise_batch_vs_oracle(rt, oracle, monkeypatch, ws):
         norm = oracle.normalise(ref)
         for unfused in (False, True):
             assert np.allclose(outs[unfused][b], norm, rtol=2e-6, atol=2e-6)
+        # the fused statistics (one-pass E[x^2] - m^2, summed in the
+        # dereddening kernel: 16-byte aligned rows) and the two-pass ones
+        # (unaligned buffers, or RIPTIDE_AMD_NORM_UNFUSED) may differ in the
+        # last bits; the bound DESIGN.md §3.3 states: <= 2e-6 x max(|x|, 1)
+        d = np.abs(outs[False][b].astype(np.float64) - outs[True][b])
+        assert np.all(d <= 2e-6 * np.maximum(np.abs(norm), 1.0)), float(d.max())
 
 
 @pytest.mark.parametrize("ws,mp", inputs.FAST_RMED_CASES)
@@ -345,6 +354,28 @@ def test_trials_per_workgroup(rt, monkeypatch, tpw, ci):
     plan = engine.PeriodogramPlan.for_search(case["n"], case["tsamp"], case["pmin"], case["pmax"],
                                              case["bmin"], case["bmax"], ducy_max=case["ducy_max"])
     xs = np.stack([inputs.with_signal(case["n"], case["tsamp"], s, case["period"], 12.0) for s in range(5)])
+    d = torch.from_numpy(xs).cuda()
+    batch = plan.run(d, check=True).cpu().numpy()
+    for b in range(5):
+        single = plan.run(d[b:b + 1].contiguous(), check=True).cpu().numpy()[0]
+        assert np.array_equal(batch[b], single), f"trial {b} differs in a batch at {tpw} trials per workgroup"
+
+
+@pytest.mark.parametrize("tpw", ["2", "16"])
+def test_trials_per_workgroup_segmented_snr(rt, monkeypatch, tpw):
+    """The trial loop over final units that run the segmented S/N:
+    cfg2 search parameters at 2^19 samples (a multi-pass schedule whose final
+    tiles of 240-260-bin rows, widths <= 9, take snr_segments), batch 5, 2 and
+    16 trials per workgroup -- every trial bit-identical to its batch-1 run,
+    so the zero-row rewrite and the next trial's fill after the S/N's maxima
+    and exchange areas leave no cross-trial state."""
+    import torch
+    from riptide_amd import engine
+    n, tsamp = 1 << 19, 256e-6
+    monkeypatch.setenv("RIPTIDE_AMD_TRIALS_PER_WG", tpw)
+    plan = engine.PeriodogramPlan.for_search(n, tsamp, 0.1, 10.0, 240, 260, ducy_max=0.05)
+    assert max(int(w) for w in plan.widths) <= 9
+    xs = np.stack([inputs.with_signal(n, tsamp, 40 + s, 0.37 + 0.2 * s, 10.0) for s in range(5)])
     d = torch.from_numpy(xs).cuda()
     batch = plan.run(d, check=True).cpu().numpy()
     for b in range(5):
@@ -550,10 +581,24 @@ def test_bench_schedule_cfg2(rt, golden_full, monkeypatch):
     _check_full_snrs(rt, g, c, one, periods, foldbins, got[0].cpu().numpy())
 
 
-@pytest.mark.parametrize("name,budget,cosched", [("cfg2", "1024", True), ("cfg2", "1536", False),
-                                                 ("cfg4", None, False), ("cfg1", None, False),
-                                                 ("cfg3", "384", False)])
-def test_full_config_every_row(rt, oracle, golden_full, monkeypatch, name, budget, cosched):
+def _trial_variants(raw, B):
+    """B distinct full-size series from the golden input:
+    the input itself (trial 0), its reversal, sign flips and circular shifts
+    -- same statistics, different S/N everywhere."""
+    n = raw.size
+    out = [raw, raw[::-1], -raw, -raw[::-1]]
+    k = 1
+    while len(out) < B:
+        sh = np.roll(raw, (k * 1048573) % n)
+        out.append(sh if k % 2 else -sh[::-1])
+        k += 1
+    return np.ascontiguousarray(np.stack(out[:B]))
+
+
+@pytest.mark.parametrize("name,budget,cosched,batch", [("cfg2", "1024", True, 16), ("cfg2", "1536", False, 1),
+                                                       ("cfg4", None, False, 16), ("cfg1", None, False, 1),
+                                                       ("cfg3", "384", True, 32)])
+def test_full_config_every_row(rt, oracle, golden_full, monkeypatch, name, budget, cosched, batch):
     """Every one of the L x W S/N values at full size (missing 3):
     the golden input through the schedule bench.py times for the config,
     compared element by element with the strict C oracle run on the same
@@ -561,7 +606,13 @@ def test_full_config_every_row(rt, oracle, golden_full, monkeypatch, name, budge
     arithmetic per step) at the 2e-6 scaled tolerance of
     test_periodogram_golden, and with the golden sampled rows / sums / peaks
     of the reference build at 1e-4.  cfg2 at 1024 M co-scheduled is
-    bench.py's schedule since round 5, at 1536 M its round-4 one."""
+    bench.py's schedule since round 5, at 1536 M its round-4 one.
+    At the benchmarked batch (cfg2 / cfg4 16 trials, cfg3
+    32 at 384 M co-scheduled) the golden input is trial 0 of a batch of
+    distinct variants, so trials 1 .. B-1 of every workgroup run the trial
+    loop's later-trial path (the next trial's fill over this trial's stores,
+    the zero-row rewrite); each of them must equal its own batch-1 run through
+    the same plan bit for bit, and trial 0 the oracle."""
     import torch
     from riptide_amd import engine
     g = golden_full["configs"][name]
@@ -573,12 +624,31 @@ def test_full_config_every_row(rt, oracle, golden_full, monkeypatch, name, budge
         monkeypatch.setenv("RIPTIDE_AMD_SCRATCH_MFLOATS", budget)
     if cosched:
         monkeypatch.setenv("RIPTIDE_AMD_COSCHED", "1")
-    plan = engine.PeriodogramPlan.for_search(c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"],
-                                             ducy_max=c["ducy_max"])
-    x = engine.deredden_normalise(torch.from_numpy(raw).cuda(), int(round(4.0 / c["tsamp"])), 101)
-    snrs = plan.run(x, check=True).cpu().numpy()
+    args = (c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"])
+    plan = engine.PeriodogramPlan.for_search(*args, ducy_max=c["ducy_max"])
+    if cosched and plan.workspace_bytes(batch) > 0.8 * torch.cuda.mem_get_info()[0]:
+        # bench.py's own fallback when the second scratch bank does not fit
+        monkeypatch.delenv("RIPTIDE_AMD_COSCHED")
+        del plan
+        plan = engine.PeriodogramPlan.for_search(*args, ducy_max=c["ducy_max"])
+    d = torch.from_numpy(_trial_variants(raw, batch)).cuda()
+    x = engine.deredden_normalise(d, int(round(4.0 / c["tsamp"])), 101)
+    del d
+    snr_dev = plan.run(x, check=True)
+    torch.cuda.synchronize()
+    if batch > 1:
+        one = torch.empty((1, plan.length, plan.num_widths), dtype=torch.float32, device="cuda")
+        ws = torch.empty(plan.workspace_bytes(1), dtype=torch.uint8, device="cuda")
+        for b in range(batch):
+            plan.run(x[b:b + 1], out=one, workspace=ws, check=True)
+            torch.cuda.synchronize()
+            nbad = int((one[0] != snr_dev[b]).sum().item())
+            assert nbad == 0, f"{name}: trial {b} of the batch of {batch}: {nbad} S/N values differ from its batch-1 run"
+        del one, ws
+    snrs = snr_dev[0].cpu().numpy()
+    del snr_dev
     periods, foldbins = plan.grid()
-    op, ofb, osnr = oracle.periodogram(x.cpu().numpy(), c["tsamp"], np.asarray(plan.widths, dtype=np.uint64),
+    op, ofb, osnr = oracle.periodogram(x[0].cpu().numpy(), c["tsamp"], np.asarray(plan.widths, dtype=np.uint64),
                                        c["pmin"], c["pmax"], c["bmin"], c["bmax"],
                                        threads=min(16, os.cpu_count() or 1))
     assert np.array_equal(periods, op) and np.array_equal(foldbins, ofb)

@@ -56,3 +56,29 @@ def test_padded_polynomial_value():
         for pv in c:
             y = y * x + pv
         assert np.array_equal(y, ref)
+
+
+def test_cluster_peaks_pipeline_order():
+    """clustering.cluster_peaks restates Pipeline.search's sort and
+    Pipeline.cluster_peaks (pipeline.py:186, 192-215): peaks sorted by
+    increasing period (stable: equal periods keep their input order), then
+    friends-of-friends in frequency at radius / Tobs -- a known answer with a
+    chain whose ends are more than one radius apart (one cluster), a gap of
+    exactly the radius (linked) and a tie in period."""
+    from riptide_amd.clustering import cluster_peaks
+    from riptide_amd.peak_detection import Peak
+    tobs, rad = 100.0, 0.2                 # radius 0.002 Hz
+    freqs = [1.0, 1.0015, 1.003, 1.0045,   # a chain: 0.0015 Hz steps, 0.0045 end to end
+             2.0, 2.002,                   # linked at exactly the radius
+             3.0, 3.0021,                  # split: 0.0021 > 0.002
+             0.5, 0.5]                     # a tie in period
+    peaks = [Peak(1.0 / f, f, 3, 0.01, 1, i, 10.0 + i, 5.0 * i) for i, f in enumerate(freqs)]
+    rs = np.random.RandomState(3)
+    shuffled = [peaks[i] for i in rs.permutation(len(peaks))]
+    ps, clusters = cluster_peaks([tuple(p) for p in shuffled], rad, tobs)
+    assert [p.period for p in ps] == sorted(p.period for p in peaks)
+    ties = [p.ip for p in ps if p.freq == 0.5]
+    assert ties == [p.ip for p in shuffled if p.freq == 0.5]          # stable sort
+    got = sorted(sorted(p.ip for p in cl) for cl in clusters)
+    assert got == [[0, 1, 2, 3], [4, 5], [6], [7], [8, 9]]
+    assert cluster_peaks([], rad, tobs) == ([], [])

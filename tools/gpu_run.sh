@@ -22,6 +22,7 @@
 #                                                    then the two SQ counter groups of the ladder kernel (first library)
 #   bash tools/gpu_run.sh TAG prep [ENV=V...]       dereddening + normalisation alone (tools/prep_bench.py) under
 #                                                    rocprofv3 --kernel-trace --stats, once per environment setting
+#   bash tools/gpu_run.sh TAG readrate [FILES]       cold-read rate of the box's storage, 1/2/4/8 readers (CPU only)
 #   bash tools/gpu_run.sh TAG round                  round-end pass: attribution (cfg2), pmc (cfg2, cfg3, cfg4),
 #                                                    tests, smoke, bench cfg2 / cfg3 / cfg5, configs, prof
 set -o pipefail
@@ -63,14 +64,14 @@ do_prof() {
   cut -c1-400 "$O/prof_json.log"
 }
 
-do_pmc() {     # $1: cfg2 (bench.py, 2 trials) or a config name (tools/ab_flags.py, 64 trials)
+do_pmc() {     # $1: cfg2 (bench.py at its batch of 16) or a config name (tools/ab_flags.py, 128 trials)
   local cfg=${1:-cfg2} d="$O/pmc_$1" i=0
   mkdir -p "$d"
   for grp in "${PMC_GROUPS[@]}"; do
     i=$((i+1))
     if [ "$cfg" = cfg2 ]; then
       (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace -f csv -d "$d/p$i" -o run \
-         -- python3 "$R/bench.py" --steps 1 --warmup 1 --batch 2 --no-cpu-baseline --no-self-check > "$d/p$i.log" 2>&1) \
+         -- python3 "$R/bench.py" --steps 1 --warmup 1 --batch 16 --no-cpu-baseline --no-self-check > "$d/p$i.log" 2>&1) \
         || fail "pmc pass $i" "$d/p$i.log"
     else
       (cd /tmp && export TMPDIR=/tmp && export AB_BATCH=16 && timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-trace -f csv -d "$d/p$i" -o run \
@@ -79,7 +80,9 @@ do_pmc() {     # $1: cfg2 (bench.py, 2 trials) or a config name (tools/ab_flags.
   done
   local out=profiles/${TAG}_pmc_cone.json
   [ "$cfg" = cfg2 ] || out=profiles/${TAG}_pmc_cone_$cfg.json
-  local per=4; [ "$cfg" = cfg2 ] || per=128     # ab_flags.py: 2 rounds x 4 runs x AB_BATCH 16 trials
+  # trials per PMC pass: bench.py at the benchmarked batch (1 warmup + 1 step x 16 trials);
+  # ab_flags.py: 2 rounds x 4 runs x AB_BATCH 16 trials
+  local per=32; [ "$cfg" = cfg2 ] || per=128
   python3 tools/pmc_to_json.py "$d" "$out" $per --config "$cfg" > "$d/json.log" 2>&1 || fail pmc_to_json "$d/json.log"
   cp "$out" "$O/"
   echo "pmc $cfg ok: $(head -c 300 "$d/json.log")"
@@ -244,6 +247,13 @@ PY
   done
 }
 
+do_readrate() {   # [FILES]: cold-read rate with 1 / 2 / 4 / 8 reader processes -> profiles/TAG_read_rate.json
+  timeout -k 10 600 python -u tools/read_rate.py "${1:-128}" "profiles/${TAG}_read_rate.json" > "$O/read_rate.log" 2>&1 \
+    || fail readrate "$O/read_rate.log"
+  cp "profiles/${TAG}_read_rate.json" "$O/"
+  grep '^readers' "$O/read_rate.log"
+}
+
 case "$CMD" in
   tests) do_tests ;;
   bench) do_bench bench "$@" ;;
@@ -262,6 +272,7 @@ case "$CMD" in
   attrib) do_attrib "$@" ;;
   ladder) do_ladder "$@" ;;
   prep) do_prep "$@" ;;
+  readrate) do_readrate "$@" ;;
   round)
     RIPTIDE_AMD_SCRATCH_MFLOATS=1024 RIPTIDE_AMD_COSCHED=1 do_attrib cfg2
     do_pmc cfg2
@@ -271,6 +282,7 @@ case "$CMD" in
     do_bench bench
     do_bench bench_cfg3 --workload cfg3
     do_bench bench_cfg5 --workload cfg5
+    do_readrate
     do_configs
     do_prof ;;
   *) echo "unknown command $CMD"; exit 2 ;;
