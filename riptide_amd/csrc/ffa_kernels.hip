@@ -2711,8 +2711,11 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
                          snr_seg_ok(p, wl[kMaxWidths], n0);
     // short rows keep their blob's LDS part at the end of the level buffer,
     // which a final pass's output level (at the S/N stride) and its S/N's
-    // dummy words may overwrite: every trial's fill then re-DMAs it
-    const bool blob_clobbered = SMAX == kPack2 && SNR;
+    // dummy words may overwrite: every trial's fill then re-DMAs it -- unless
+    // the output level at the short-row S/N stride ends below the blob (set
+    // below: that stride takes the S/N's whole-chunk path, which writes no
+    // dummy words, only the rows [0, n0 q) and their wrapped extensions)
+    bool blob_clobbered = SMAX == kPack2 && SNR;
     // short rows in (row, segment) tasks: every level above the fill at the
     // odd stride pack_stride(p)
     if constexpr (SMAX == kPack2) {
@@ -2724,6 +2727,10 @@ __global__ __launch_bounds__(kConeBlock, kConeWavesPerSimd) void cone_kernel(Con
         if (SNR && L > 0 && p >= kPackSeg && (a.flags & kConeSnrStride)) {
             const int qf = snr_short_stride(p);
             if (n0 * qf <= kLdsDataFloats) qout = qf;
+            // the blob survives the S/N: loaded once per workgroup, not per
+            // trial (cfg4's final units re-read ~12 KB of
+            // blob per trial, 0.1 GB of its 1.34 GB)
+            if (qout == qf && n0 * qf + U.run_off <= kLdsBufFloats) blob_clobbered = false;
         }
     }
     if constexpr (SMAX <= 5 && SMAX != kPack2) {

@@ -247,11 +247,14 @@ PY
   done
 }
 
-do_readrate() {   # [FILES]: cold-read rate with 1 / 2 / 4 / 8 reader processes -> profiles/TAG_read_rate.json
-  timeout -k 10 600 python -u tools/read_rate.py "${1:-128}" "profiles/${TAG}_read_rate.json" > "$O/read_rate.log" 2>&1 \
-    || fail readrate "$O/read_rate.log"
-  cp "profiles/${TAG}_read_rate.json" "$O/"
-  grep '^readers' "$O/read_rate.log"
+do_readrate() {   # [FILES]: cold-read rate with 1 / 2 / 4 / 8 reader processes -> profiles/TAG_read_rate.jsonl
+  # /tmp (bench.py cfg5's files without TMPDIR) and the repo's own file system
+  mkdir -p "$O/rr"
+  timeout -k 10 600 python -u tools/read_rate.py "${1:-128}" "profiles/${TAG}_read_rate.jsonl" /tmp "$O/rr" \
+    > "$O/read_rate.log" 2>&1 || fail readrate "$O/read_rate.log"
+  rm -rf "$O/rr"
+  cp "profiles/${TAG}_read_rate.jsonl" "$O/"
+  grep 'readers' "$O/read_rate.log"
 }
 
 case "$CMD" in

@@ -10,7 +10,7 @@ for each reader count drops them from the page cache (POSIX_FADV_DONTNEED)
 and times R processes reading disjoint round-robin shares with readinto()
 into a reused buffer (bench.py's page-locked slots are filled the same way).
 
-usage: python tools/read_rate.py [FILES] [OUT.json]
+usage: python tools/read_rate.py [FILES] [OUT.jsonl] [DIR...]   (default DIR: $TMPDIR or /tmp)
 """
 import json
 import multiprocessing as mp
@@ -33,6 +33,22 @@ def _drop(fn):
         os.close(fd)
 
 
+def _fs_type(path):
+    """(mount point, fs type, source) of the mount holding path (/proc/mounts,
+    longest prefix): tmpfs / overlay on RAM make 'cold' reads page-cache reads."""
+    best = ("", "?", "?")
+    p = os.path.realpath(path)
+    try:
+        with open("/proc/mounts") as f:
+            for line in f:
+                src, mnt, typ = line.split()[:3]
+                if (p == mnt or p.startswith(mnt.rstrip("/") + "/")) and len(mnt) > len(best[0]):
+                    best = (mnt, typ, src)
+    except OSError:
+        pass
+    return best
+
+
 def _reader(fnames, start_evt, q):
     buf = bytearray(CHUNK)
     mv = memoryview(buf)
@@ -52,7 +68,14 @@ def _reader(fnames, start_evt, q):
 def main():
     nfiles = int(sys.argv[1]) if len(sys.argv) > 1 else 64
     out = sys.argv[2] if len(sys.argv) > 2 else ""
-    root = os.environ.get("TMPDIR", "/tmp")
+    roots = sys.argv[3:] or [os.environ.get("TMPDIR", "/tmp")]
+    lines = [measure(nfiles, root) for root in roots]
+    if out:
+        with open(out, "w") as f:
+            f.write("".join(json.dumps(x) + "\n" for x in lines))
+
+
+def measure(nfiles, root):
     need = nfiles * (33 << 20)
     free = shutil.disk_usage(root).free
     if need > 0.8 * free:
@@ -70,7 +93,9 @@ def main():
             fnames.append(fn)
         del blob32
         total = sum(os.path.getsize(f) for f in fnames)
+        mnt, typ, src = _fs_type(root)
         res = {"files": nfiles, "bytes": total, "mean_file_mib": total / nfiles / 2**20, "root": root,
+               "mount": mnt, "fs_type": typ, "fs_source": src,
                "cpus_affinity": len(os.sched_getaffinity(0)), "readers": {}}
         ctx = mp.get_context("spawn")
         for R in (1, 2, 4, 8):
@@ -90,12 +115,10 @@ def main():
             nb = sum(g[0] for g in got)
             res["readers"][str(R)] = {"GiB_per_s": nb / wall / 2**30, "files_per_s": nfiles / wall,
                                       "seconds": wall}
-            print(f"readers {R}: {nb / wall / 2**30:.2f} GiB/s, {nfiles / wall:.1f} files/s", flush=True)
-        line = json.dumps(res)
-        print(line, flush=True)
-        if out:
-            with open(out, "w") as f:
-                f.write(line + "\n")
+            print(f"{root} ({typ}) readers {R}: {nb / wall / 2**30:.2f} GiB/s, {nfiles / wall:.1f} files/s",
+                  flush=True)
+        print(json.dumps(res), flush=True)
+        return res
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
