@@ -1126,6 +1126,7 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
             const int qb = 2 * q + 1 < RW ? 2 * q + 1 : RW - 1;   // row B's register row (q < Q: in range)
             if (2 * q + 1 < RW) {
                 if (kq == kSlotPair) {
+#ifdef RT_PAIR_SELECT
                     int n0[SMAX];
 #pragma unroll
                     for (int k = 0; k < SMAX; ++k) n0[k] = __builtin_amdgcn_readlane(__float_as_int(ts[(k + 1) % SMAX]), 0);
@@ -1136,6 +1137,30 @@ __device__ __forceinline__ void merge_step_slots(const UnitCtx& C, const float* 
                         x = lane == (k + 1 < SMAX ? 63 : jl) ? __int_as_float(n0[k]) : x;
                         v[qb][k] = __fadd_rn(hs[k], x);
                     }
+#else
+                    // bin j + 1 of the rolled tail term: slot k's lanes 0-62
+                    // from lanes 1-63 (wave_shl:1, bound_ctrl off: lane 63 has
+                    // no source and keeps the old value), lane 63 from lane 0
+                    // of slot k + 1 (the old value: wave_rol:1 of slot k + 1);
+                    // the last slot's bin p - 1 (lane jl) takes bin 0 (lane 0
+                    // of slot 0) by v_writelane -- two or three VALU per slot
+                    // instead of a v_readlane, a move and a select each
+                    const int w0 = __builtin_amdgcn_readlane(__float_as_int(ts[0]), 0);
+#pragma unroll
+                    for (int k = 0; k < SMAX; ++k) {
+                        int x;
+                        if (k + 1 < SMAX) {
+                            const int nx = __builtin_amdgcn_mov_dpp(__float_as_int(ts[k + 1]), 0x134, 0xF, 0xF, false);
+                            x = __builtin_amdgcn_update_dpp(nx, __float_as_int(ts[k]), 0x130, 0xF, 0xF, false);
+                        } else {
+                            x = __builtin_amdgcn_mov_dpp(__float_as_int(ts[k]), 0x130, 0xF, 0xF, true);
+                            // lane select in M0 (gfx9: one SGPR operand per VALU instruction)
+                            asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(x) : "s"(w0), "s"(jl)
+                                         : "m0");
+                        }
+                        v[qb][k] = __fadd_rn(hs[k], __int_as_float(x));
+                    }
+#endif
                 } else if (kq == kSlotHalf) {
                     // row B shares row A's head term: only its tail term
                     float tb[SMAX];
