@@ -55,7 +55,10 @@ def test_ffa2_golden_bit_exact(rt, golden, m, p, seed):
                                  # short rows: every interleaved-task segment count (p = 9-32) with p
                                  # a multiple of 8 and not (bins past p land in the row padding)
                                  (999, 9), (1500, 12), (5000, 20), (4099, 24), (2049, 27), (3001, 31),
-                                 (65537, 32)])
+                                 (65537, 32),
+                                 # 5-slot rows: through the roll table (257-260 bins: one and four
+                                 # fifth-slot bins) and without it (261-320)
+                                 (3001, 257), (2999, 260), (4099, 261), (2000, 300), (1000, 320)])
 def test_ffa2_vs_oracle(rt, oracle, m, p):
     x = np.random.RandomState(m * 31 + p).normal(size=(m, p)).astype(np.float32)
     assert np.array_equal(rt.ffa2(x), oracle.ffa2(x))
