@@ -137,97 +137,227 @@ __device__ __forceinline__ void ds_rung_range(const DsRung& r, uint64_t s0, uint
 // - start is (floor(start) + 1.0) - start exactly, end - imax is end -
 // min(floor(end), N - 1)), and each rung's output range in the span is
 // computed once per block by one lane per rung instead of by every thread.
-__global__ __launch_bounds__(256) void downsample_fused_kernel(
+//
+// The span is staged as overlapping pairs: pair i holds samples s0 + i and
+// s0 + i + 1, 8-byte aligned, so a window's consecutive samples from ANY
+// start come in ds_read_b64 reads at immediate offsets (2 LDS cycles per 64
+// lanes x 2 samples, 64 banks) -- with single samples (ds_read_b32 or the
+// compiler's ds_read2_b32, 32 banks) the reads took twice the LDS cycles
+// and, the window starts of adjacent outputs lying f apart, conflicted
+// alike (tools/ladder_conflicts.py).  Volatile reads: the
+// compiler would fuse two of them into ds_read2_b64 (8 cycles).
+typedef float ds_pair __attribute__((ext_vector_type(2), aligned(8)));
+// 512 threads: the 32 KiB of pairs allow four workgroups per CU, eight waves
+// each (RT_DS_THREADS: geometry A/B builds)
+#ifndef RT_DS_THREADS
+#define RT_DS_THREADS 512
+#endif
+constexpr uint32_t kDsFusedThreads = RT_DS_THREADS;
+static_assert((kDsFusedThreads & (kDsFusedThreads - 1)) == 0 && kDsFusedThreads >= 64, "whole waves, power of two");
+typedef const volatile __attribute__((address_space(3))) ds_pair* ds_pptr;
+
+__global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
     const float* __restrict__ x, uint64_t n_in, uint64_t x_stride,
     const DsRung* __restrict__ rungs, uint32_t num_rungs,
     float* __restrict__ out, uint64_t out_stride)
 {
-    __shared__ float span[kDsSpanFloats];
+    __shared__ ds_pair pairs[kDsSpanFloats];
     __shared__ uint32_t kr[2 * kDsMaxRungs];
     const uint64_t s0 = (uint64_t)blockIdx.x * kDsFusedSpan;
     const uint64_t s_end = min(s0 + (uint64_t)kDsFusedSpan, n_in);     // window starts owned by this block
     const uint64_t l_end = min(s0 + (uint64_t)kDsSpanFloats, n_in);    // staged input
     x += (uint64_t)blockIdx.y * x_stride;
     out += (uint64_t)blockIdx.y * out_stride;
-    for (uint64_t i = s0 + threadIdx.x; i < l_end; i += 256) span[i - s0] = x[i];
-    for (uint32_t ri = threadIdx.x; ri < num_rungs; ri += 256) {
+    // Only a block staged up to the end of the series can hold windows that
+    // min(floor(end), N - 1) clips (otherwise end < s_end + margin <= l_end
+    // < N); every other block stages all kDsSpanFloats pairs, sample
+    // s0 + kDsSpanFloats included.  Its loads go out together, ahead of the
+    // rung ranges (one lane per rung: scalar float64 divisions and loops),
+    // so the two latencies overlap.
+    const bool tail = l_end >= n_in;
+    static_assert(kDsMaxRungs <= kDsFusedThreads, "one lane per rung");
+    const bool has_rung = threadIdx.x < num_rungs;
+    DsRung rr{};
+    if (has_rung) rr = rungs[threadIdx.x];
+    constexpr uint32_t SU = kDsSpanFloats / kDsFusedThreads;
+    float sa[SU], sb[SU];
+    if (!tail) {
+        const float* xs = x + s0 + threadIdx.x;
+#pragma unroll
+        for (uint32_t u = 0; u < SU; ++u) {
+            sa[u] = xs[u * kDsFusedThreads];
+            sb[u] = xs[u * kDsFusedThreads + 1];
+        }
+    }
+    if (has_rung) {
         uint32_t a, b;
-        ds_rung_range(rungs[ri], s0, s_end, n_in, a, b);
-        kr[2 * ri] = a;
-        kr[2 * ri + 1] = b;
+        ds_rung_range(rr, s0, s_end, n_in, a, b);
+        kr[2 * threadIdx.x] = a;
+        kr[2 * threadIdx.x + 1] = b;
+    }
+    if (!tail) {
+#pragma unroll
+        for (uint32_t u = 0; u < SU; ++u) pairs[threadIdx.x + u * kDsFusedThreads] = ds_pair{sa[u], sb[u]};
+    } else {
+        for (uint64_t i = s0 + threadIdx.x; i < l_end; i += kDsFusedThreads)
+            pairs[i - s0] = ds_pair{x[i], i + 1 < n_in ? x[i + 1] : 0.0f};
     }
     __syncthreads();
     const double last = (double)n_in - 1.0;
     const uint32_t b0 = (uint32_t)s0;
-    // Only a block staged up to the end of the series can hold windows that
-    // min(floor(end), N - 1) clips (otherwise end < s_end + margin <= l_end
-    // < N).  Every other block has cnt >= floor(f) (floor and rounding are
-    // monotone and start + floor(f) is exact), so with CC = floor(f) + 1 its
-    // reads w[1 .. CC - 2] all add and only w[CC - 1] depends on cnt; the
-    // clipping block takes the general window sum.
-    const bool tail = l_end >= n_in;
-    // one output k of a rung of factor f: window_sum or, with CC > 0 (f <
-    // CC), the window's reads w[0 .. CC) at immediate offsets, w[CC - 1]
-    // adding -0.0 (an exact no-op) when cnt = CC - 1, instead of window_sum's groups of
-    // eight (at f ~ 1.5, most of the ladder's outputs: 8 reads, selects and
-    // adds for 1-2 terms).  cnt <= floor(f) + 1: reads w[0 .. floor(f)],
-    // inside the staged margin (kDsFusedMargin >= ceil(f) + 2).
-    auto output = [&](auto cc, double f, uint32_t k) -> float {
-        constexpr int CC = decltype(cc)::value;
+    // lp[s]: the pair of sample s (pointer arithmetic, so the compiler folds
+    // a window's pair offsets into the reads' immediate offsets)
+    const ds_pptr lp = (ds_pptr)pairs - b0;
+    // A non-clipping block has cnt = floor(f) or floor(f) + 1 (floor and
+    // rounding are monotone and start + floor(f) is exact), so with F =
+    // floor(f) its samples w[1 .. F - 1] all add, w[F] adds when cnt = F + 1
+    // (else -0.0, an exact no-op) and w[cnt] is a select of w[F] and w[F + 1]
+    // (inside the staged margin: kDsFusedMargin >= ceil(f) + 2); the clipping
+    // block takes the general sum.  The non-clipping bounds come from fract
+    // and truncation: (floor(start) + 1) - start is 1 - frac(start) rounded
+    // once, as 1.0 - fract(start) is (fract is exact for start >= 0);
+    // end - floor(end) is fract(end) exactly (Sterbenz); the uint32
+    // truncations are the floors.
+    //
+    // F < 12 (most of the ladder's outputs: f ~ 1.5-10 at cfg2): one template
+    // instance per F, every read at an immediate offset.
+    auto output_small = [&](auto ff, double f, uint32_t k) -> float {
+        constexpr int F = decltype(ff)::value;
+        const double start = __dmul_rn((double)k, f);
+        const double end = __dadd_rn(start, f);
+        const uint32_t imin = (uint32_t)start, imax = (uint32_t)end;
+        const float wmin = (float)__dsub_rn(1.0, __builtin_amdgcn_fract(start));
+        const float wmax = (float)__builtin_amdgcn_fract(end);
+        const bool full = imax - imin > (uint32_t)F;
+        const ds_pptr w = lp + imin;
+        float v[F + 3];
+#pragma unroll
+        for (int j = 0; j <= F + 1; j += 2) {
+            const ds_pair q = w[j];
+            v[j] = q.x;
+            v[j + 1] = q.y;
+        }
+        float acc = __fmul_rn(wmin, v[0]);
+#pragma unroll
+        for (int j = 1; j < F; ++j) acc = __fadd_rn(acc, v[j]);
+        acc = __fadd_rn(acc, full ? v[F] : -0.0f);
+        return __fadd_rn(acc, __fmul_rn(wmax, full ? v[F + 1] : v[F]));
+    };
+    // F >= 12: the same sum with uniform trip counts (F is the rung's), four
+    // pair reads ahead of their eight additions
+    auto output_large = [&](double f, uint32_t F, uint32_t k) -> float {
+        const double start = __dmul_rn((double)k, f);
+        const double end = __dadd_rn(start, f);
+        const uint32_t imin = (uint32_t)start, imax = (uint32_t)end;
+        const float wmin = (float)__dsub_rn(1.0, __builtin_amdgcn_fract(start));
+        const float wmax = (float)__builtin_amdgcn_fract(end);
+        const bool full = imax - imin > F;
+        const ds_pptr w = lp + imin;
+        ds_pair q = w[0];
+        float acc = __fadd_rn(__fmul_rn(wmin, q.x), q.y);
+        uint32_t e = 2;
+        for (; e + 8 <= F; e += 8) {
+            ds_pair g[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) g[i] = w[e + 2 * i];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc = __fadd_rn(__fadd_rn(acc, g[i].x), g[i].y);
+        }
+        for (; e + 2 <= F; e += 2) {
+            q = w[e];
+            acc = __fadd_rn(__fadd_rn(acc, q.x), q.y);
+        }
+        if (e < F) acc = __fadd_rn(acc, w[e].x);
+        q = w[F];
+        acc = __fadd_rn(acc, full ? q.x : -0.0f);
+        return __fadd_rn(acc, __fmul_rn(wmax, full ? q.y : q.x));
+    };
+    // the clipping block: the reference's bounds with min(floor(end), N - 1)
+    // and the window sum sample by sample
+    auto output_tail = [&](double f, uint32_t k) -> float {
         const double start = __dmul_rn((double)k, f);
         const double end = __dadd_rn(start, f);
         const double fs = floor(start);
         double dmax = floor(end);
-        if (CC == 0 && dmax > last) dmax = last;
+        if (dmax > last) dmax = last;
         const uint32_t imin = (uint32_t)fs, imax = (uint32_t)dmax;
         const float wmin = (float)__dsub_rn(__dadd_rn(fs, 1.0), start);
         const float wmax = (float)__dsub_rn(end, dmax);
-        const float* w = span + (imin - b0);
-        const uint32_t cnt = imax - imin;
-        float acc;
-        if constexpr (CC > 0) {
-            float v[CC];
-#pragma unroll
-            for (int j = 0; j < CC; ++j) v[j] = w[j];
-            acc = __fmul_rn(wmin, v[0]);
-#pragma unroll
-            for (int j = 1; j < CC - 1; ++j) acc = __fadd_rn(acc, v[j]);
-            acc = __fadd_rn(acc, (uint32_t)(CC - 1) < cnt ? v[CC - 1] : -0.0f);
-        } else {
-            acc = window_sum(w, wmin, cnt);
-        }
-        return __fadd_rn(acc, __fmul_rn(wmax, w[cnt]));
+        const ds_pptr w = lp + imin;
+        float acc = __fmul_rn(wmin, w[0].x);
+        for (uint32_t j = 1; j < imax - imin; ++j) acc = __fadd_rn(acc, w[j].x);
+        return __fadd_rn(acc, __fmul_rn(wmax, w[imax - imin].x));
     };
-    for (uint32_t ri = 0; ri < num_rungs; ++ri) {
-        const DsRung r = rungs[ri];
-        float* o = out + r.out_off;
-        const uint32_t k_lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)kr[2 * ri]);
-        const uint32_t k_hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)kr[2 * ri + 1]);
-        if (r.identity) {
-            for (uint32_t k = k_lo + threadIdx.x; k < k_hi; k += 256) o[k] = span[k - b0];
-            continue;
-        }
-        const double f = r.f;
-        auto rung = [&](auto cc) {
-            for (uint32_t k = k_lo + threadIdx.x; k < k_hi; k += 256) o[k] = output(cc, f, k);
-        };
-        if (tail) {
-            rung(IntC<0>{});
-            continue;
-        }
-        switch ((int)f + 1) {
-        case 2: rung(IntC<2>{}); break;
-        case 3: rung(IntC<3>{}); break;
-        case 4: rung(IntC<4>{}); break;
-        case 5: rung(IntC<5>{}); break;
-        case 6: rung(IntC<6>{}); break;
-        case 7: rung(IntC<7>{}); break;
-        case 8: rung(IntC<8>{}); break;
-        case 9: rung(IntC<9>{}); break;
-        case 10: rung(IntC<10>{}); break;
-        case 11: rung(IntC<11>{}); break;
-        case 12: rung(IntC<12>{}); break;
-        default: rung(IntC<0>{}); break;
+    // the rung table in lanes: lane l of every wave holds rung c + l's output
+    // range and parameters (one LDS read and one global load per 64 rungs),
+    // taken per rung with v_readlane -- a per-rung LDS read and scalar load
+    // were a memory wait per rung and wave (57 rungs at cfg2)
+    const uint32_t lane = threadIdx.x & 63;
+    // Work balance: the rungs' outputs tile the waves in turn -- output
+    // k_lo + i of a rung goes to thread (rot + i) mod T, rot advancing by
+    // each rung's output count rounded up to whole waves -- so the short
+    // rungs (f > 7: fewer than T outputs in a span) land on successive waves
+    // instead of all on the first ones, and the workgroup's waves finish
+    // together (its LDS frees for the next one only when the last does).  A
+    // wave's lanes stay consecutive outputs; a wave without outputs in a
+    // rung skips it on scalar compares.
+    const uint32_t wbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u));
+    uint32_t rot = 0;
+    for (uint32_t c = 0; c < num_rungs; c += 64) {
+        const uint32_t rl = min(c + lane, num_rungs - 1);
+        const int my_lo = (int)kr[2 * rl], my_hi = (int)kr[2 * rl + 1];
+        const DsRung mr = rungs[rl];
+        const long long my_f = __double_as_longlong(mr.f);
+        const int my_f_lo = (int)(uint32_t)my_f, my_f_hi = (int)(uint32_t)((uint64_t)my_f >> 32);
+        const int my_o_lo = (int)(uint32_t)mr.out_off, my_o_hi = (int)(uint32_t)(mr.out_off >> 32);
+        const int my_id = (int)mr.identity;
+        const uint32_t nr = min(64u, num_rungs - c);
+        for (uint32_t j = 0; j < nr; ++j) {
+            const uint32_t k_lo = (uint32_t)__builtin_amdgcn_readlane(my_lo, (int)j);
+            const uint32_t k_hi = (uint32_t)__builtin_amdgcn_readlane(my_hi, (int)j);
+            const uint32_t nk = k_hi - k_lo;
+            const uint32_t wfirst = (wbase - rot) & (kDsFusedThreads - 1);
+            const uint32_t i0 = (threadIdx.x - rot) & (kDsFusedThreads - 1);
+            rot = (rot + ((nk + 63) & ~63u)) & (kDsFusedThreads - 1);
+            if (wfirst >= nk) continue;          // rot: a multiple of 64
+            const uint64_t off = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(my_o_lo, (int)j) |
+                                 ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(my_o_hi, (int)j) << 32);
+            float* o = out + off;
+            if (__builtin_amdgcn_readlane(my_id, (int)j)) {
+                for (uint32_t k = k_lo + i0; k < k_hi; k += kDsFusedThreads) o[k] = lp[k].x;
+                continue;
+            }
+            const double f = __longlong_as_double(
+                (long long)((uint64_t)(uint32_t)__builtin_amdgcn_readlane(my_f_lo, (int)j) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(my_f_hi, (int)j) << 32)));
+            if (tail) {
+                for (uint32_t k = k_lo + i0; k < k_hi; k += kDsFusedThreads) o[k] = output_tail(f, k);
+                continue;
+            }
+            auto rung = [&](auto ff) {
+                for (uint32_t k = k_lo + i0; k < k_hi; k += kDsFusedThreads) o[k] = output_small(ff, f, k);
+            };
+            const uint32_t F = (uint32_t)f;
+            switch (F) {
+            case 1: rung(IntC<1>{}); break;
+            case 2: rung(IntC<2>{}); break;
+            case 3: rung(IntC<3>{}); break;
+            case 4: rung(IntC<4>{}); break;
+            case 5: rung(IntC<5>{}); break;
+            case 6: rung(IntC<6>{}); break;
+            case 7: rung(IntC<7>{}); break;
+            case 8: rung(IntC<8>{}); break;
+            case 9: rung(IntC<9>{}); break;
+            case 10: rung(IntC<10>{}); break;
+            case 11: rung(IntC<11>{}); break;
+            default:
+                // F >= 12 (F = 0 does not occur: f > 1 off the identity rung)
+                if (F >= 12)
+                    for (uint32_t k = k_lo + i0; k < k_hi; k += kDsFusedThreads) o[k] = output_large(f, F, k);
+                else
+                    for (uint32_t k = k_lo + i0; k < k_hi; k += kDsFusedThreads) o[k] = output_tail(f, k);
+                break;
+            }
         }
     }
 }
@@ -237,7 +367,7 @@ hipError_t launch_downsample_fused(const float* x, uint64_t n_in, uint64_t x_str
 {
     if (!num_rungs || !batch || !n_in) return hipSuccess;
     const uint64_t blocks = (n_in + kDsFusedSpan - 1) / kDsFusedSpan;
-    hipLaunchKernelGGL(downsample_fused_kernel, dim3((uint32_t)blocks, batch), dim3(256), 0, s, x, n_in, x_stride,
+    hipLaunchKernelGGL(downsample_fused_kernel, dim3((uint32_t)blocks, batch), dim3(kDsFusedThreads), 0, s, x, n_in, x_stride,
                        d_rungs, num_rungs, out, out_stride);
     return hipGetLastError();
 }

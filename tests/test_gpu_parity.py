@@ -509,6 +509,33 @@ def test_fused_ladder_matches_per_rung(monkeypatch):
         assert np.array_equal(outs[0], outs[1])
 
 
+def test_fused_ladder_leaves_match_per_rung(monkeypatch):
+    """The fused ladder's leaves themselves (every rung's downsampled series,
+    the workspace's leaf buffer after plan.ladder) equal the per-rung kernel's
+    bit for bit: cfg2's full-size 57-rung ladder, the margin edge case and a
+    short odd-length series (the clipping tail block)."""
+    import torch
+    from riptide_amd import engine
+    cases = [dict(n=1 << 23, tsamp=256e-6, pmin=0.1, pmax=10.0, bmin=240, bmax=260, ducy_max=0.2),
+             inputs.LADDER_EDGE_CASE, dict(inputs.PGRAM_CASES[1], n=inputs.PGRAM_CASES[1]["n"] - 37),
+             inputs.PGRAM_CASES[3]]
+    for case in cases:
+        x = torch.from_numpy(np.random.RandomState(11).normal(size=(2, case["n"])).astype(np.float32)).cuda()
+        leaves = []
+        for per_rung in (False, True):
+            if per_rung:
+                monkeypatch.setenv("RIPTIDE_AMD_PER_RUNG_LADDER", "1")
+            else:
+                monkeypatch.delenv("RIPTIDE_AMD_PER_RUNG_LADDER", raising=False)
+            plan = engine.PeriodogramPlan.for_search(case["n"], case["tsamp"], case["pmin"], case["pmax"],
+                                                     case["bmin"], case["bmax"], ducy_max=case["ducy_max"])
+            ws = torch.zeros(plan.workspace_bytes(2), dtype=torch.uint8, device="cuda")
+            plan.ladder(x, ws)
+            torch.cuda.synchronize()
+            leaves.append(ws)
+        assert torch.equal(leaves[0], leaves[1]), case
+
+
 # ---------------------------------------------------------------- full-size BASELINE configs
 @pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3", "cfg4"])
 def test_full_config(rt, golden_full, name):
