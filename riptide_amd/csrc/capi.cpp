@@ -599,7 +599,7 @@ struct rt_plan {
 namespace {
 
 // The fused ladder (downsample_fused_kernel) indexes samples and outputs in
-// 32 bits and stages kDsFusedMargin floats past each span: series of 2^29
+// 32 bits and stages up to kDsFusedMargin floats past each span: series of 2^29
 // samples or more, rungs whose window (ceil(f) + 2) exceeds the margin, and
 // more rungs than its per-block table take the per-rung kernel (64-bit
 // indices) instead.
@@ -607,9 +607,7 @@ constexpr uint64_t kDsFusedMaxSize = 1ull << 29;
 bool ladder_fusable(size_t size, const std::vector<DsRung>& rungs)
 {
     if ((uint64_t)size >= kDsFusedMaxSize || rungs.size() > kDsMaxRungs) return false;
-    for (const DsRung& d : rungs)
-        if (!d.identity && std::ceil(d.f) + 2.0 > (double)kDsFusedMargin) return false;
-    return true;
+    return ds_fused_margin(rungs.data(), rungs.size()) != 0;
 }
 
 // The rungs of a periodogram that feed at least one transform, in the
@@ -738,8 +736,9 @@ void run_ladder(const rt_plan* P, const float* d_data, size_t batch, size_t data
         ck(hipEventRecord(r.a, s), "hipEventRecord");
     }
     if (P->ds_fused)
-        ck(launch_downsample_fused(d_data, P->pg.prm.size, data_stride, P->d_rungs, (uint32_t)P->rungs.size(), leaves,
-                                   P->pg.leaf_floats, (uint32_t)batch, s),
+        ck(launch_downsample_fused(d_data, P->pg.prm.size, data_stride, P->d_rungs, (uint32_t)P->rungs.size(),
+                                   ds_fused_margin(P->rungs.data(), P->rungs.size()), leaves, P->pg.leaf_floats,
+                                   (uint32_t)batch, s),
            "downsample_fused");
     else
         ck(launch_downsample_ladder(d_data, P->pg.prm.size, data_stride, P->d_rungs, (uint32_t)P->rungs.size(),

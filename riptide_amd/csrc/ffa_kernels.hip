@@ -101,12 +101,12 @@ __global__ __launch_bounds__(256) void downsample_ladder_kernel(
     out[k] = __fadd_rn(window_sum(w, wmin, cnt), __fmul_rn(wmax, w[cnt]));
 }
 
-// Fused ladder: one block per input span (and trial) computes the outputs of
-// EVERY rung whose window starts in the span, so the series is read from HBM
-// once instead of once per rung (57 rungs at cfg2).  The span plus a margin
-// of kDsFusedMargin floats (>= ceil(f) + 2 for every fused rung) is staged in
-// LDS; each output is the same sequential window sum as the per-rung kernel.
-constexpr uint32_t kDsFusedSpan = kDsSpanFloats - kDsFusedMargin;
+// Fused ladder: one block per input span (and trial pair) computes the
+// outputs of EVERY rung whose window starts in the span, so the series is
+// read from HBM once instead of once per rung (57 rungs at cfg2).  The span
+// plus a margin (the plan's: ceil(f) + 2 for its largest fused rung, rounded
+// up to 64, <= kDsFusedMargin) is staged in LDS, kDsSpanFloats samples in
+// all; each output is the same sequential window sum as the per-rung kernel.
 
 // first output k of a rung whose window start floor(k f) is >= s
 __device__ __forceinline__ uint64_t ds_first_output(double f, uint64_t s)
@@ -147,27 +147,38 @@ __device__ __forceinline__ void ds_rung_range(const DsRung& r, uint64_t s0, uint
 // alike (tools/ladder_conflicts.py).  Volatile reads: the
 // compiler would fuse two of them into ds_read2_b64 (8 cycles).
 typedef float ds_pair __attribute__((ext_vector_type(2), aligned(8)));
-// 512 threads: the 32 KiB of pairs allow four workgroups per CU, eight waves
-// each (RT_DS_THREADS: geometry A/B builds)
+// A workgroup runs NT = 2 trials of one span: each output's float64 bounds
+// (most of the VALU work at f < 12) are computed once for both trials'
+// windows.  1024 threads: 2 x 32 KiB of pairs allow two workgroups per CU,
+// sixteen waves each (the CU's 32; 512 threads left it half full).
+// RT_DS_THREADS / RT_DS_TRIALS: geometry A/B builds.
 #ifndef RT_DS_THREADS
-#define RT_DS_THREADS 512
+#define RT_DS_THREADS 1024
+#endif
+#ifndef RT_DS_TRIALS
+#define RT_DS_TRIALS 2
 #endif
 constexpr uint32_t kDsFusedThreads = RT_DS_THREADS;
+constexpr uint32_t kDsFusedTrials = RT_DS_TRIALS;
 static_assert((kDsFusedThreads & (kDsFusedThreads - 1)) == 0 && kDsFusedThreads >= 64, "whole waves, power of two");
+static_assert(kDsFusedTrials == 1 || kDsFusedTrials == 2, "trials per workgroup");
 typedef const volatile __attribute__((address_space(3))) ds_pair* ds_pptr;
 
 __global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
     const float* __restrict__ x, uint64_t n_in, uint64_t x_stride,
     const DsRung* __restrict__ rungs, uint32_t num_rungs,
-    float* __restrict__ out, uint64_t out_stride)
+    float* __restrict__ out, uint64_t out_stride, uint32_t batch, uint32_t span)
 {
-    __shared__ ds_pair pairs[kDsSpanFloats];
+    constexpr uint32_t NT = kDsFusedTrials;
+    __shared__ ds_pair pairs[NT * kDsSpanFloats];
     __shared__ uint32_t kr[2 * kDsMaxRungs];
-    const uint64_t s0 = (uint64_t)blockIdx.x * kDsFusedSpan;
-    const uint64_t s_end = min(s0 + (uint64_t)kDsFusedSpan, n_in);     // window starts owned by this block
+    const uint64_t s0 = (uint64_t)blockIdx.x * span;
+    const uint64_t s_end = min(s0 + (uint64_t)span, n_in);             // window starts owned by this block
     const uint64_t l_end = min(s0 + (uint64_t)kDsSpanFloats, n_in);    // staged input
-    x += (uint64_t)blockIdx.y * x_stride;
-    out += (uint64_t)blockIdx.y * out_stride;
+    // trials t0 .. t0 + nt - 1 (a last workgroup of an odd batch stages its
+    // one trial twice and stores the same values twice)
+    const uint32_t t0 = blockIdx.y * NT;
+    const uint32_t nt = min(NT, batch - t0);
     // Only a block staged up to the end of the series can hold windows that
     // min(floor(end), N - 1) clips (otherwise end < s_end + margin <= l_end
     // < N); every other block stages all kDsSpanFloats pairs, sample
@@ -180,13 +191,16 @@ __global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
     DsRung rr{};
     if (has_rung) rr = rungs[threadIdx.x];
     constexpr uint32_t SU = kDsSpanFloats / kDsFusedThreads;
-    float sa[SU], sb[SU];
+    float sa[NT][SU], sb[NT][SU];
     if (!tail) {
-        const float* xs = x + s0 + threadIdx.x;
 #pragma unroll
-        for (uint32_t u = 0; u < SU; ++u) {
-            sa[u] = xs[u * kDsFusedThreads];
-            sb[u] = xs[u * kDsFusedThreads + 1];
+        for (uint32_t q = 0; q < NT; ++q) {
+            const float* xs = x + (uint64_t)(t0 + min(q, nt - 1)) * x_stride + s0 + threadIdx.x;
+#pragma unroll
+            for (uint32_t u = 0; u < SU; ++u) {
+                sa[q][u] = xs[u * kDsFusedThreads];
+                sb[q][u] = xs[u * kDsFusedThreads + 1];
+            }
         }
     }
     if (has_rung) {
@@ -197,22 +211,29 @@ __global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
     }
     if (!tail) {
 #pragma unroll
-        for (uint32_t u = 0; u < SU; ++u) pairs[threadIdx.x + u * kDsFusedThreads] = ds_pair{sa[u], sb[u]};
+        for (uint32_t q = 0; q < NT; ++q)
+#pragma unroll
+            for (uint32_t u = 0; u < SU; ++u)
+                pairs[q * kDsSpanFloats + threadIdx.x + u * kDsFusedThreads] = ds_pair{sa[q][u], sb[q][u]};
     } else {
-        for (uint64_t i = s0 + threadIdx.x; i < l_end; i += kDsFusedThreads)
-            pairs[i - s0] = ds_pair{x[i], i + 1 < n_in ? x[i + 1] : 0.0f};
+        for (uint32_t q = 0; q < NT; ++q) {
+            const float* xq = x + (uint64_t)(t0 + min(q, nt - 1)) * x_stride;
+            for (uint64_t i = s0 + threadIdx.x; i < l_end; i += kDsFusedThreads)
+                pairs[q * kDsSpanFloats + (i - s0)] = ds_pair{xq[i], i + 1 < n_in ? xq[i + 1] : 0.0f};
+        }
     }
     __syncthreads();
     const double last = (double)n_in - 1.0;
     const uint32_t b0 = (uint32_t)s0;
-    // lp[s]: the pair of sample s (pointer arithmetic, so the compiler folds
-    // a window's pair offsets into the reads' immediate offsets)
+    // lp[s] (+ q kDsSpanFloats for trial q): the pair of sample s (pointer
+    // arithmetic, so the compiler folds a window's pair offsets, and the
+    // second trial's 32 KiB, into the reads' immediate offsets)
     const ds_pptr lp = (ds_pptr)pairs - b0;
     // A non-clipping block has cnt = floor(f) or floor(f) + 1 (floor and
     // rounding are monotone and start + floor(f) is exact), so with F =
     // floor(f) its samples w[1 .. F - 1] all add, w[F] adds when cnt = F + 1
     // (else -0.0, an exact no-op) and w[cnt] is a select of w[F] and w[F + 1]
-    // (inside the staged margin: kDsFusedMargin >= ceil(f) + 2); the clipping
+    // (inside the staged margin: the plan's >= ceil(f) + 2); the clipping
     // block takes the general sum.  The non-clipping bounds come from fract
     // and truncation: (floor(start) + 1) - start is 1 - frac(start) rounded
     // once, as 1.0 - fract(start) is (fract is exact for start >= 0);
@@ -221,61 +242,91 @@ __global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
     //
     // F < 12 (most of the ladder's outputs: f ~ 1.5-10 at cfg2): one template
     // instance per F, every read at an immediate offset.
-    auto output_small = [&](auto ff, double f, uint32_t k) -> float {
+    // trial q's rung output (a missing second trial: the first's, whose
+    // values it recomputes from the same staged samples -- no branch)
+    float* oq[NT];
+    // vo: the output's byte offset (32 bits: a rung holds < 2^29 outputs),
+    // one offset for both trials' stores (global_store with an SGPR base)
+    auto put = [&](uint32_t q, uint32_t vo, float v) { *(float*)((char*)oq[q] + vo) = v; };
+    // kd: the output index k as float64 (exact), the window start's operand
+    auto output_small = [&](auto ff, double f, double kd, uint32_t vo) {
         constexpr int F = decltype(ff)::value;
-        const double start = __dmul_rn((double)k, f);
+        const double start = __dmul_rn(kd, f);
         const double end = __dadd_rn(start, f);
         const uint32_t imin = (uint32_t)start, imax = (uint32_t)end;
         const float wmin = (float)__dsub_rn(1.0, __builtin_amdgcn_fract(start));
         const float wmax = (float)__builtin_amdgcn_fract(end);
         const bool full = imax - imin > (uint32_t)F;
         const ds_pptr w = lp + imin;
-        float v[F + 3];
+        // every read of both trials first (volatile reads issue in program
+        // order), then the two independent sums
+        float v[NT][F + 3];
 #pragma unroll
-        for (int j = 0; j <= F + 1; j += 2) {
-            const ds_pair q = w[j];
-            v[j] = q.x;
-            v[j + 1] = q.y;
+        for (uint32_t q = 0; q < NT; ++q)
+#pragma unroll
+            for (int j = 0; j <= F + 1; j += 2) {
+                const ds_pair p = w[q * kDsSpanFloats + j];
+                v[q][j] = p.x;
+                v[q][j + 1] = p.y;
+            }
+#pragma unroll
+        for (uint32_t q = 0; q < NT; ++q) {
+            float acc = __fmul_rn(wmin, v[q][0]);
+#pragma unroll
+            for (int j = 1; j < F; ++j) acc = __fadd_rn(acc, v[q][j]);
+            acc = __fadd_rn(acc, full ? v[q][F] : -0.0f);
+            put(q, vo, __fadd_rn(acc, __fmul_rn(wmax, full ? v[q][F + 1] : v[q][F])));
         }
-        float acc = __fmul_rn(wmin, v[0]);
-#pragma unroll
-        for (int j = 1; j < F; ++j) acc = __fadd_rn(acc, v[j]);
-        acc = __fadd_rn(acc, full ? v[F] : -0.0f);
-        return __fadd_rn(acc, __fmul_rn(wmax, full ? v[F + 1] : v[F]));
     };
     // F >= 12: the same sum with uniform trip counts (F is the rung's), four
     // pair reads ahead of their eight additions
-    auto output_large = [&](double f, uint32_t F, uint32_t k) -> float {
-        const double start = __dmul_rn((double)k, f);
+    auto output_large = [&](double f, uint32_t F, double kd, uint32_t vo) {
+        const double start = __dmul_rn(kd, f);
         const double end = __dadd_rn(start, f);
         const uint32_t imin = (uint32_t)start, imax = (uint32_t)end;
         const float wmin = (float)__dsub_rn(1.0, __builtin_amdgcn_fract(start));
         const float wmax = (float)__builtin_amdgcn_fract(end);
         const bool full = imax - imin > F;
         const ds_pptr w = lp + imin;
-        ds_pair q = w[0];
-        float acc = __fadd_rn(__fmul_rn(wmin, q.x), q.y);
+        // both trials' sums side by side (independent chains)
+        float acc[NT];
+#pragma unroll
+        for (uint32_t q = 0; q < NT; ++q) {
+            const ds_pair p = w[q * kDsSpanFloats];
+            acc[q] = __fadd_rn(__fmul_rn(wmin, p.x), p.y);
+        }
         uint32_t e = 2;
         for (; e + 8 <= F; e += 8) {
-            ds_pair g[4];
+            ds_pair g[NT][4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) g[i] = w[e + 2 * i];
+            for (uint32_t q = 0; q < NT; ++q)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) acc = __fadd_rn(__fadd_rn(acc, g[i].x), g[i].y);
+                for (int i = 0; i < 4; ++i) g[q][i] = w[q * kDsSpanFloats + e + 2 * i];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (uint32_t q = 0; q < NT; ++q) acc[q] = __fadd_rn(__fadd_rn(acc[q], g[q][i].x), g[q][i].y);
         }
-        for (; e + 2 <= F; e += 2) {
-            q = w[e];
-            acc = __fadd_rn(__fadd_rn(acc, q.x), q.y);
+        for (; e + 2 <= F; e += 2)
+#pragma unroll
+            for (uint32_t q = 0; q < NT; ++q) {
+                const ds_pair p = w[q * kDsSpanFloats + e];
+                acc[q] = __fadd_rn(__fadd_rn(acc[q], p.x), p.y);
+            }
+        if (e < F)
+#pragma unroll
+            for (uint32_t q = 0; q < NT; ++q) acc[q] = __fadd_rn(acc[q], w[q * kDsSpanFloats + e].x);
+#pragma unroll
+        for (uint32_t q = 0; q < NT; ++q) {
+            const ds_pair p = w[q * kDsSpanFloats + F];
+            const float a = __fadd_rn(acc[q], full ? p.x : -0.0f);
+            put(q, vo, __fadd_rn(a, __fmul_rn(wmax, full ? p.y : p.x)));
         }
-        if (e < F) acc = __fadd_rn(acc, w[e].x);
-        q = w[F];
-        acc = __fadd_rn(acc, full ? q.x : -0.0f);
-        return __fadd_rn(acc, __fmul_rn(wmax, full ? q.y : q.x));
     };
     // the clipping block: the reference's bounds with min(floor(end), N - 1)
     // and the window sum sample by sample
-    auto output_tail = [&](double f, uint32_t k) -> float {
-        const double start = __dmul_rn((double)k, f);
+    auto output_tail = [&](double f, double kd, uint32_t vo) {
+        const double start = __dmul_rn(kd, f);
         const double end = __dadd_rn(start, f);
         const double fs = floor(start);
         double dmax = floor(end);
@@ -283,10 +334,12 @@ __global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
         const uint32_t imin = (uint32_t)fs, imax = (uint32_t)dmax;
         const float wmin = (float)__dsub_rn(__dadd_rn(fs, 1.0), start);
         const float wmax = (float)__dsub_rn(end, dmax);
-        const ds_pptr w = lp + imin;
-        float acc = __fmul_rn(wmin, w[0].x);
-        for (uint32_t j = 1; j < imax - imin; ++j) acc = __fadd_rn(acc, w[j].x);
-        return __fadd_rn(acc, __fmul_rn(wmax, w[imax - imin].x));
+        for (uint32_t q = 0; q < NT; ++q) {
+            const ds_pptr w = lp + q * kDsSpanFloats + imin;
+            float acc = __fmul_rn(wmin, w[0].x);
+            for (uint32_t j = 1; j < imax - imin; ++j) acc = __fadd_rn(acc, w[j].x);
+            put(q, vo, __fadd_rn(acc, __fmul_rn(wmax, w[imax - imin].x)));
+        }
     };
     // the rung table in lanes: lane l of every wave holds rung c + l's output
     // range and parameters (one LDS read and one global load per 64 rungs),
@@ -322,20 +375,31 @@ __global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
             if (wfirst >= nk) continue;          // rot: a multiple of 64
             const uint64_t off = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(my_o_lo, (int)j) |
                                  ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(my_o_hi, (int)j) << 32);
-            float* o = out + off;
+#pragma unroll
+            for (uint32_t q = 0; q < NT; ++q) oq[q] = out + (uint64_t)(t0 + min(q, nt - 1)) * out_stride + off;
             if (__builtin_amdgcn_readlane(my_id, (int)j)) {
-                for (uint32_t k = k_lo + i0; k < k_hi; k += kDsFusedThreads) o[k] = lp[k].x;
+                for (uint32_t k = k_lo + i0; k < k_hi; k += kDsFusedThreads)
+#pragma unroll
+                    for (uint32_t q = 0; q < NT; ++q) put(q, 4u * k, lp[q * kDsSpanFloats + k].x);
                 continue;
             }
             const double f = __longlong_as_double(
                 (long long)((uint64_t)(uint32_t)__builtin_amdgcn_readlane(my_f_lo, (int)j) |
                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(my_f_hi, (int)j) << 32)));
+            // this thread's outputs k = k_lo + i0, + T, ... < k_hi of the rung, as
+            // (k as float64, byte offset 4 k): the loop runs on those two alone
+            auto outputs = [&](auto body) {
+                const double kend = (double)k_hi;
+                double kd = (double)(k_lo + i0);
+                for (uint32_t vo = 4u * (k_lo + i0); kd < kend; kd += (double)kDsFusedThreads, vo += 4u * kDsFusedThreads)
+                    body(kd, vo);
+            };
             if (tail) {
-                for (uint32_t k = k_lo + i0; k < k_hi; k += kDsFusedThreads) o[k] = output_tail(f, k);
+                outputs([&](double kd, uint32_t vo) { output_tail(f, kd, vo); });
                 continue;
             }
             auto rung = [&](auto ff) {
-                for (uint32_t k = k_lo + i0; k < k_hi; k += kDsFusedThreads) o[k] = output_small(ff, f, k);
+                outputs([&](double kd, uint32_t vo) { output_small(ff, f, kd, vo); });
             };
             const uint32_t F = (uint32_t)f;
             switch (F) {
@@ -353,9 +417,9 @@ __global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
             default:
                 // F >= 12 (F = 0 does not occur: f > 1 off the identity rung)
                 if (F >= 12)
-                    for (uint32_t k = k_lo + i0; k < k_hi; k += kDsFusedThreads) o[k] = output_large(f, F, k);
+                    outputs([&](double kd, uint32_t vo) { output_large(f, F, kd, vo); });
                 else
-                    for (uint32_t k = k_lo + i0; k < k_hi; k += kDsFusedThreads) o[k] = output_tail(f, k);
+                    outputs([&](double kd, uint32_t vo) { output_tail(f, kd, vo); });
                 break;
             }
         }
@@ -363,12 +427,16 @@ __global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
 }
 
 hipError_t launch_downsample_fused(const float* x, uint64_t n_in, uint64_t x_stride, const DsRung* d_rungs,
-                                   uint32_t num_rungs, float* out, uint64_t out_stride, uint32_t batch, hipStream_t s)
+                                   uint32_t num_rungs, uint32_t margin, float* out, uint64_t out_stride,
+                                   uint32_t batch, hipStream_t s)
 {
     if (!num_rungs || !batch || !n_in) return hipSuccess;
-    const uint64_t blocks = (n_in + kDsFusedSpan - 1) / kDsFusedSpan;
-    hipLaunchKernelGGL(downsample_fused_kernel, dim3((uint32_t)blocks, batch), dim3(kDsFusedThreads), 0, s, x, n_in, x_stride,
-                       d_rungs, num_rungs, out, out_stride);
+    if (margin < 2 || margin > kDsFusedMargin) return hipErrorInvalidValue;
+    const uint32_t span = kDsSpanFloats - margin;
+    const uint64_t blocks = (n_in + span - 1) / span;
+    hipLaunchKernelGGL(downsample_fused_kernel, dim3((uint32_t)blocks, (batch + kDsFusedTrials - 1) / kDsFusedTrials),
+                       dim3(kDsFusedThreads), 0, s, x, n_in, x_stride, d_rungs, num_rungs, out, out_stride, batch,
+                       span);
     return hipGetLastError();
 }
 

@@ -41,9 +41,24 @@ inline void ds_configure(DsRung& r)
 hipError_t launch_downsample_ladder(const float* x, uint64_t n_in, uint64_t x_stride,
                                     const DsRung* d_rungs, uint32_t num_rungs, uint32_t total_blocks,
                                     float* out, uint64_t out_stride, uint32_t batch, hipStream_t s);
-// all rungs of a periodogram from one read of the series (every rung: ceil(f) + 2 <= kDsFusedMargin)
+// all rungs of a periodogram from one read of the series; margin: samples
+// staged past each span, ds_fused_margin(rungs) (every rung: ceil(f) + 2 <= margin <= kDsFusedMargin)
 hipError_t launch_downsample_fused(const float* x, uint64_t n_in, uint64_t x_stride, const DsRung* d_rungs,
-                                   uint32_t num_rungs, float* out, uint64_t out_stride, uint32_t batch, hipStream_t s);
+                                   uint32_t num_rungs, uint32_t margin, float* out, uint64_t out_stride,
+                                   uint32_t batch, hipStream_t s);
+
+// The fused ladder's margin for a plan's rungs: ceil(f) + 2 of the largest
+// non-identity rung, rounded up to 64 samples (0: a rung needs more than
+// kDsFusedMargin -- not fusable).
+inline uint32_t ds_fused_margin(const DsRung* rungs, size_t num_rungs)
+{
+    double need = 2.0;
+    for (size_t i = 0; i < num_rungs; ++i)
+        if (!rungs[i].identity) need = std::fmax(need, std::ceil(rungs[i].f) + 2.0);
+    if (need > (double)kDsFusedMargin) return 0;
+    const uint32_t m = ((uint32_t)need + 63u) & ~63u;
+    return m < kDsFusedMargin ? m : kDsFusedMargin;
+}
 // smax: merge_slots() bucket covering every transform of the launch
 hipError_t launch_cone(const ConeArgs& args, uint32_t smax, uint32_t rw, bool wide_snr, bool snr,
                        hipStream_t s);   // grid (num_items, batch); rw, wide_snr, snr: the Launch's
