@@ -117,18 +117,13 @@ __device__ __forceinline__ uint64_t ds_first_output(double f, uint64_t s)
     return k;
 }
 
-// Outputs [k_lo, k_hi) of a rung whose window start floor(k f) lies in
-// [s0, s_end) (the block's span; s_end = n_in for the last block).
-__device__ __forceinline__ void ds_rung_range(const DsRung& r, uint64_t s0, uint64_t s_end, uint64_t n_in,
-                                              uint32_t& k_lo, uint32_t& k_hi)
+// The first output of a rung whose window start floor(k f) is >= s, clipped
+// to the rung's length: k_lo of a block's span [s0, s_end) at s = s0, k_hi
+// at s = s_end (s_end = n_in for the last block: every remaining output).
+__device__ __forceinline__ uint32_t ds_rung_bound(const DsRung& r, uint64_t s, uint64_t n_in)
 {
-    if (r.identity) {
-        k_lo = (uint32_t)min(s0, r.n);
-        k_hi = (uint32_t)min(s_end, r.n);
-        return;
-    }
-    k_lo = (uint32_t)min(ds_first_output(r.f, s0), r.n);
-    k_hi = (uint32_t)min(s_end >= n_in ? r.n : ds_first_output(r.f, s_end), r.n);
+    if (r.identity) return (uint32_t)min(s, r.n);
+    return (uint32_t)(s >= n_in ? r.n : min(ds_first_output(r.f, s), r.n));
 }
 
 // Every rung's window sums over one staged span.  Indices are 32-bit (the
@@ -183,13 +178,14 @@ __global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
     // min(floor(end), N - 1) clips (otherwise end < s_end + margin <= l_end
     // < N); every other block stages all kDsSpanFloats pairs, sample
     // s0 + kDsSpanFloats included.  Its loads go out together, ahead of the
-    // rung ranges (one lane per rung: scalar float64 divisions and loops),
-    // so the two latencies overlap.
+    // rung ranges (one lane per rung bound, k_lo and k_hi in two waves:
+    // float64 divisions and loops), so the two latencies overlap.
     const bool tail = l_end >= n_in;
-    static_assert(kDsMaxRungs <= kDsFusedThreads, "one lane per rung");
-    const bool has_rung = threadIdx.x < num_rungs;
+    static_assert(2 * kDsMaxRungs <= kDsFusedThreads, "one lane per rung bound");
+    const uint32_t r_hi = threadIdx.x / kDsMaxRungs, r_i = threadIdx.x % kDsMaxRungs;
+    const bool has_rung = r_hi < 2 && r_i < num_rungs;
     DsRung rr{};
-    if (has_rung) rr = rungs[threadIdx.x];
+    if (has_rung) rr = rungs[r_i];
     constexpr uint32_t SU = kDsSpanFloats / kDsFusedThreads;
     float sa[NT][SU], sb[NT][SU];
     if (!tail) {
@@ -203,12 +199,7 @@ __global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
             }
         }
     }
-    if (has_rung) {
-        uint32_t a, b;
-        ds_rung_range(rr, s0, s_end, n_in, a, b);
-        kr[2 * threadIdx.x] = a;
-        kr[2 * threadIdx.x + 1] = b;
-    }
+    if (has_rung) kr[2 * r_i + r_hi] = ds_rung_bound(rr, r_hi ? s_end : s0, n_in);
     if (!tail) {
 #pragma unroll
         for (uint32_t q = 0; q < NT; ++q)
