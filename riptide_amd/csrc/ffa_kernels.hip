@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256) void downsample_ladder_kernel(
 // outputs of EVERY rung whose window starts in the span, so the series is
 // read from HBM once instead of once per rung (57 rungs at cfg2).  The span
 // plus a margin (the plan's: ceil(f) + 2 for its largest fused rung, rounded
-// up to 64, <= kDsFusedMargin) is staged in LDS, kDsSpanFloats samples in
+// up to 64, <= kDsFusedMargin) is staged in LDS, kDsPairSpan samples in
 // all; each output is the same sequential window sum as the per-rung kernel.
 
 // first output k of a rung whose window start floor(k f) is >= s
@@ -157,6 +157,15 @@ constexpr uint32_t kDsFusedThreads = RT_DS_THREADS;
 constexpr uint32_t kDsFusedTrials = RT_DS_TRIALS;
 static_assert((kDsFusedThreads & (kDsFusedThreads - 1)) == 0 && kDsFusedThreads >= 64, "whole waves, power of two");
 static_assert(kDsFusedTrials == 1 || kDsFusedTrials == 2, "trials per workgroup");
+// samples staged per trial (pairs): two trials' pairs and the rung table fill
+// just under half the CU's 160 KiB, so two workgroups stay resident
+// (RT_DS_PAIRS: A/B builds)
+#ifndef RT_DS_PAIRS
+#define RT_DS_PAIRS 4864
+#endif
+constexpr uint32_t kDsPairSpan = RT_DS_PAIRS;
+static_assert(kDsPairSpan >= 4 * kDsFusedMargin && kDsPairSpan % 64 == 0, "span: whole waves, margin <= a quarter");
+static_assert(2 * (kDsFusedTrials * kDsPairSpan * 8 + 8 * kDsMaxRungs) <= 160 * 1024, "two workgroups per CU");
 typedef const volatile __attribute__((address_space(3))) ds_pair* ds_pptr;
 
 __global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
@@ -165,19 +174,19 @@ __global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
     float* __restrict__ out, uint64_t out_stride, uint32_t batch, uint32_t span)
 {
     constexpr uint32_t NT = kDsFusedTrials;
-    __shared__ ds_pair pairs[NT * kDsSpanFloats];
+    __shared__ ds_pair pairs[NT * kDsPairSpan];
     __shared__ uint32_t kr[2 * kDsMaxRungs];
     const uint64_t s0 = (uint64_t)blockIdx.x * span;
     const uint64_t s_end = min(s0 + (uint64_t)span, n_in);             // window starts owned by this block
-    const uint64_t l_end = min(s0 + (uint64_t)kDsSpanFloats, n_in);    // staged input
+    const uint64_t l_end = min(s0 + (uint64_t)kDsPairSpan, n_in);    // staged input
     // trials t0 .. t0 + nt - 1 (a last workgroup of an odd batch stages its
     // one trial twice and stores the same values twice)
     const uint32_t t0 = blockIdx.y * NT;
     const uint32_t nt = min(NT, batch - t0);
     // Only a block staged up to the end of the series can hold windows that
     // min(floor(end), N - 1) clips (otherwise end < s_end + margin <= l_end
-    // < N); every other block stages all kDsSpanFloats pairs, sample
-    // s0 + kDsSpanFloats included.  Its loads go out together, ahead of the
+    // < N); every other block stages all kDsPairSpan pairs, sample
+    // s0 + kDsPairSpan included.  Its loads go out together, ahead of the
     // rung ranges (one lane per rung bound, k_lo and k_hi in two waves:
     // float64 divisions and loops), so the two latencies overlap.
     const bool tail = l_end >= n_in;
@@ -186,7 +195,7 @@ __global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
     const bool has_rung = r_hi < 2 && r_i < num_rungs;
     DsRung rr{};
     if (has_rung) rr = rungs[r_i];
-    constexpr uint32_t SU = kDsSpanFloats / kDsFusedThreads;
+    constexpr uint32_t SU = (kDsPairSpan + kDsFusedThreads - 1) / kDsFusedThreads;
     float sa[NT][SU], sb[NT][SU];
     if (!tail) {
 #pragma unroll
@@ -194,8 +203,10 @@ __global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
             const float* xs = x + (uint64_t)(t0 + min(q, nt - 1)) * x_stride + s0 + threadIdx.x;
 #pragma unroll
             for (uint32_t u = 0; u < SU; ++u) {
-                sa[q][u] = xs[u * kDsFusedThreads];
-                sb[q][u] = xs[u * kDsFusedThreads + 1];
+                if (kDsPairSpan % kDsFusedThreads == 0 || threadIdx.x + u * kDsFusedThreads < kDsPairSpan) {
+                    sa[q][u] = xs[u * kDsFusedThreads];
+                    sb[q][u] = xs[u * kDsFusedThreads + 1];
+                }
             }
         }
     }
@@ -205,18 +216,19 @@ __global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
         for (uint32_t q = 0; q < NT; ++q)
 #pragma unroll
             for (uint32_t u = 0; u < SU; ++u)
-                pairs[q * kDsSpanFloats + threadIdx.x + u * kDsFusedThreads] = ds_pair{sa[q][u], sb[q][u]};
+                if (kDsPairSpan % kDsFusedThreads == 0 || threadIdx.x + u * kDsFusedThreads < kDsPairSpan)
+                    pairs[q * kDsPairSpan + threadIdx.x + u * kDsFusedThreads] = ds_pair{sa[q][u], sb[q][u]};
     } else {
         for (uint32_t q = 0; q < NT; ++q) {
             const float* xq = x + (uint64_t)(t0 + min(q, nt - 1)) * x_stride;
             for (uint64_t i = s0 + threadIdx.x; i < l_end; i += kDsFusedThreads)
-                pairs[q * kDsSpanFloats + (i - s0)] = ds_pair{xq[i], i + 1 < n_in ? xq[i + 1] : 0.0f};
+                pairs[q * kDsPairSpan + (i - s0)] = ds_pair{xq[i], i + 1 < n_in ? xq[i + 1] : 0.0f};
         }
     }
     __syncthreads();
     const double last = (double)n_in - 1.0;
     const uint32_t b0 = (uint32_t)s0;
-    // lp[s] (+ q kDsSpanFloats for trial q): the pair of sample s (pointer
+    // lp[s] (+ q kDsPairSpan for trial q): the pair of sample s (pointer
     // arithmetic, so the compiler folds a window's pair offsets, and the
     // second trial's 32 KiB, into the reads' immediate offsets)
     const ds_pptr lp = (ds_pptr)pairs - b0;
@@ -256,7 +268,7 @@ __global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
         for (uint32_t q = 0; q < NT; ++q)
 #pragma unroll
             for (int j = 0; j <= F + 1; j += 2) {
-                const ds_pair p = w[q * kDsSpanFloats + j];
+                const ds_pair p = w[q * kDsPairSpan + j];
                 v[q][j] = p.x;
                 v[q][j + 1] = p.y;
             }
@@ -283,7 +295,7 @@ __global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
         float acc[NT];
 #pragma unroll
         for (uint32_t q = 0; q < NT; ++q) {
-            const ds_pair p = w[q * kDsSpanFloats];
+            const ds_pair p = w[q * kDsPairSpan];
             acc[q] = __fadd_rn(__fmul_rn(wmin, p.x), p.y);
         }
         uint32_t e = 2;
@@ -292,7 +304,7 @@ __global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
 #pragma unroll
             for (uint32_t q = 0; q < NT; ++q)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) g[q][i] = w[q * kDsSpanFloats + e + 2 * i];
+                for (int i = 0; i < 4; ++i) g[q][i] = w[q * kDsPairSpan + e + 2 * i];
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -301,15 +313,15 @@ __global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
         for (; e + 2 <= F; e += 2)
 #pragma unroll
             for (uint32_t q = 0; q < NT; ++q) {
-                const ds_pair p = w[q * kDsSpanFloats + e];
+                const ds_pair p = w[q * kDsPairSpan + e];
                 acc[q] = __fadd_rn(__fadd_rn(acc[q], p.x), p.y);
             }
         if (e < F)
 #pragma unroll
-            for (uint32_t q = 0; q < NT; ++q) acc[q] = __fadd_rn(acc[q], w[q * kDsSpanFloats + e].x);
+            for (uint32_t q = 0; q < NT; ++q) acc[q] = __fadd_rn(acc[q], w[q * kDsPairSpan + e].x);
 #pragma unroll
         for (uint32_t q = 0; q < NT; ++q) {
-            const ds_pair p = w[q * kDsSpanFloats + F];
+            const ds_pair p = w[q * kDsPairSpan + F];
             const float a = __fadd_rn(acc[q], full ? p.x : -0.0f);
             put(q, vo, __fadd_rn(a, __fmul_rn(wmax, full ? p.y : p.x)));
         }
@@ -326,7 +338,7 @@ __global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
         const float wmin = (float)__dsub_rn(__dadd_rn(fs, 1.0), start);
         const float wmax = (float)__dsub_rn(end, dmax);
         for (uint32_t q = 0; q < NT; ++q) {
-            const ds_pptr w = lp + q * kDsSpanFloats + imin;
+            const ds_pptr w = lp + q * kDsPairSpan + imin;
             float acc = __fmul_rn(wmin, w[0].x);
             for (uint32_t j = 1; j < imax - imin; ++j) acc = __fadd_rn(acc, w[j].x);
             put(q, vo, __fadd_rn(acc, __fmul_rn(wmax, w[imax - imin].x)));
@@ -371,7 +383,7 @@ __global__ __launch_bounds__(kDsFusedThreads) void downsample_fused_kernel(
             if (__builtin_amdgcn_readlane(my_id, (int)j)) {
                 for (uint32_t k = k_lo + i0; k < k_hi; k += kDsFusedThreads)
 #pragma unroll
-                    for (uint32_t q = 0; q < NT; ++q) put(q, 4u * k, lp[q * kDsSpanFloats + k].x);
+                    for (uint32_t q = 0; q < NT; ++q) put(q, 4u * k, lp[q * kDsPairSpan + k].x);
                 continue;
             }
             const double f = __longlong_as_double(
@@ -423,7 +435,7 @@ hipError_t launch_downsample_fused(const float* x, uint64_t n_in, uint64_t x_str
 {
     if (!num_rungs || !batch || !n_in) return hipSuccess;
     if (margin < 2 || margin > kDsFusedMargin) return hipErrorInvalidValue;
-    const uint32_t span = kDsSpanFloats - margin;
+    const uint32_t span = kDsPairSpan - margin;
     const uint64_t blocks = (n_in + span - 1) / span;
     hipLaunchKernelGGL(downsample_fused_kernel, dim3((uint32_t)blocks, (batch + kDsFusedTrials - 1) / kDsFusedTrials),
                        dim3(kDsFusedThreads), 0, s, x, n_in, x_stride, d_rungs, num_rungs, out, out_stride, batch,
