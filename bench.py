@@ -65,21 +65,25 @@ def pmc_traffic(workload="cfg2"):
     summary of this workload (profiles/*_pmc_cone.json for cfg2,
     profiles/*_pmc_cone_<cfg>.json for the others; written by
     tools/pmc_to_json.py from rocprofv3 FETCH_SIZE/WRITE_SIZE passes).
-    Returns (summary or None, reason): a summary measured on other kernel
-    sources than these (`csrc_sha` != source_digest()) is stale and not used."""
+    Returns (summary or None, reason): the newest summary measured on these
+    kernel sources (`csrc_sha` == source_digest()); one measured on other
+    sources is stale and not used."""
     import glob
     pat = "*_pmc_cone.json" if workload == "cfg2" else f"*_pmc_cone_{workload}.json"
     files = sorted(glob.glob(os.path.join(REPO, "profiles", pat)))   # r01a < r01b < ...: newest last
     if not files:
         return None, f"no {workload} PMC summary under profiles/"
+    cur = source_digest()
+    for fn in reversed(files):
+        with open(fn) as f:
+            d = json.load(f)
+        if d.get("csrc_sha") == cur:
+            return {"hbm_bytes_per_trial": d["hbm_bytes_per_trial"], "source": os.path.relpath(fn, REPO),
+                    "commit": d.get("commit")}, "ok"
     with open(files[-1]) as f:
         d = json.load(f)
-    src = os.path.relpath(files[-1], REPO)
-    cur = source_digest()
-    if d.get("csrc_sha") != cur:
-        return None, (f"stale: {src} was measured on kernel sources {d.get('csrc_sha') or d.get('commit')}, "
-                      f"these are {cur}")
-    return {"hbm_bytes_per_trial": d["hbm_bytes_per_trial"], "source": src, "commit": d.get("commit")}, "ok"
+    return None, (f"stale: {os.path.relpath(files[-1], REPO)} (the newest) was measured on kernel sources "
+                  f"{d.get('csrc_sha') or d.get('commit')}, these are {cur}; no summary matches")
 
 
 def cpu_baseline(workload="cfg2", cores="", extra=(), timeout_s=400):

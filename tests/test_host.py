@@ -340,3 +340,30 @@ def test_asan_schedule_check():
         assert r.returncode == 0, (name, r.returncode, r.stdout, r.stderr[-3000:])
         if name == "cfg2-bench-1536M":
             assert int(r.stdout.split("launches=")[1].split()[0]) <= 16, r.stdout
+
+
+def test_bench_pmc_summary_matches_sources(tmp_path, monkeypatch):
+    """bench.pmc_traffic takes the newest PMC summary measured on the current
+    kernel sources (csrc_sha == source_digest()), not merely the newest file
+    name, and reports the traffic as stale when none matches."""
+    import json
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    (tmp_path / "riptide_amd" / "csrc").mkdir(parents=True)
+    (tmp_path / "riptide_amd" / "csrc" / "k.hip").write_text("kernel v1")
+    (tmp_path / "profiles").mkdir()
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    cur = bench.source_digest()
+
+    def put(name, sha, hbm):
+        (tmp_path / "profiles" / name).write_text(json.dumps({"csrc_sha": sha, "hbm_bytes_per_trial": hbm}))
+
+    put("r06a_pmc_cone.json", "0123", 1.0)
+    put("r06f_pmc_cone.json", cur, 2.0)
+    put("r06z_pmc_cone.json", "4567", 3.0)           # newest name, other sources
+    s, why = bench.pmc_traffic("cfg2")
+    assert why == "ok" and s["hbm_bytes_per_trial"] == 2.0 and s["source"].endswith("r06f_pmc_cone.json")
+    put("r06f_pmc_cone_cfg3.json", "0123", 1.0)
+    s, why = bench.pmc_traffic("cfg3")
+    assert s is None and why.startswith("stale")
