@@ -115,9 +115,10 @@ int rt_schedule_check(size_t size, double tsamp, size_t num_widths, double perio
 /* Host-only: the downsampling-ladder kernel a periodogram plan of these
  * parameters runs (periodogram.hpp:162-168 restated per rung): *fused = 1
  * for the one-read fused ladder (32-bit sample indices: series below 2^29
- * samples, every rung's window inside its staging margin), 0 for the
- * per-rung kernel (64-bit indices); *rungs = rungs that feed a transform.
- * Either pointer may be NULL. */
+ * samples, every rung's window inside its staging margin), 2 for the fused
+ * ladder over the rungs inside the margin plus the per-rung kernel for the
+ * wider ones, 0 for the per-rung kernel alone (64-bit indices); *rungs =
+ * rungs that feed a transform.  Either pointer may be NULL. */
 int rt_ladder_check(size_t size, double tsamp, double period_min, double period_max, size_t bins_min,
                     size_t bins_max, int* fused, uint64_t* rungs);
 

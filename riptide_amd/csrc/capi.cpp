@@ -586,11 +586,20 @@ struct rt_plan {
     std::vector<DsRung> rungs;
     DsRung* d_rungs = nullptr;
     uint32_t ds_blocks = 0;
-    bool ds_fused = false;   // every rung fits the fused ladder's margin
+    // kLadderPerRung / kLadderFused (every rung fits the fused ladder's
+    // margin) / kLadderHybrid (the rungs that fit take the fused kernel, the
+    // wider ones the per-rung kernel: rungs_w, first_block within the subset)
+    int ds_mode = 0;
+    std::vector<DsRung> rungs_f, rungs_w;
+    DsRung* d_rungs_f = nullptr;
+    DsRung* d_rungs_w = nullptr;
+    uint32_t ds_blocks_w = 0;
     int* d_flag = nullptr;   // sticky device error flag of the cone kernel (rt_plan_check reads and clears it)
     ~rt_plan()
     {
         if (d_rungs) (void)hipFree(d_rungs);
+        if (d_rungs_f) (void)hipFree(d_rungs_f);
+        if (d_rungs_w) (void)hipFree(d_rungs_w);
         if (d_widths) (void)hipFree(d_widths);
         if (d_flag) (void)hipFree(d_flag);
     }
@@ -604,10 +613,35 @@ namespace {
 // more rungs than its per-block table take the per-rung kernel (64-bit
 // indices) instead.
 constexpr uint64_t kDsFusedMaxSize = 1ull << 29;
-bool ladder_fusable(size_t size, const std::vector<DsRung>& rungs)
+constexpr int kLadderPerRung = 0, kLadderFused = 1, kLadderHybrid = 2;
+
+bool rung_fusable(const DsRung& d) { return d.identity || std::ceil(d.f) + 2.0 <= (double)kDsFusedMargin; }
+
+// The ladder's kernels for a plan's rungs: every rung in the fused kernel;
+// or, when some rungs' windows exceed its margin (cfg5's long range: factors
+// up to ~1950), the others in the fused kernel and those in the per-rung
+// kernel (hybrid, `f` / `w` the two subsets, w's first_block renumbered);
+// or all per-rung (series of 2^29 samples or more: 32-bit indices; more
+// fusable rungs than the fused kernel's per-block table).
+int ladder_split(size_t size, const std::vector<DsRung>& rungs, std::vector<DsRung>* f, std::vector<DsRung>* w)
 {
-    if ((uint64_t)size >= kDsFusedMaxSize || rungs.size() > kDsMaxRungs) return false;
-    return ds_fused_margin(rungs.data(), rungs.size()) != 0;
+    if ((uint64_t)size >= kDsFusedMaxSize) return kLadderPerRung;
+    std::vector<DsRung> a, b;
+    uint32_t blocks = 0;
+    for (const DsRung& d : rungs) {
+        if (rung_fusable(d)) {
+            a.push_back(d);
+        } else {
+            DsRung e = d;
+            e.first_block = blocks;
+            blocks += (uint32_t)((e.n + e.per_block - 1) / e.per_block);
+            b.push_back(e);
+        }
+    }
+    if (a.empty() || a.size() > kDsMaxRungs || ds_fused_margin(a.data(), a.size()) == 0) return kLadderPerRung;
+    if (f) *f = a;
+    if (w) *w = b;
+    return b.empty() ? kLadderFused : kLadderHybrid;
 }
 
 // The rungs of a periodogram that feed at least one transform, in the
@@ -680,11 +714,18 @@ rt_plan* make_plan(size_t size, double tsamp, const uint64_t* widths, size_t nw,
         P->rungs = used_rungs(P->pg);
         P->ds_blocks = 0;
         for (const DsRung& d : P->rungs) P->ds_blocks += (uint32_t)((d.n + d.per_block - 1) / d.per_block);
-        P->ds_fused = !std::getenv("RIPTIDE_AMD_PER_RUNG_LADDER") && ladder_fusable(prm.size, P->rungs);
-        ck(hipMalloc(&P->d_rungs, std::max<size_t>(1, P->rungs.size()) * sizeof(DsRung)), "hipMalloc");
-        if (!P->rungs.empty())
-            ck(hipMemcpy(P->d_rungs, P->rungs.data(), P->rungs.size() * sizeof(DsRung), hipMemcpyHostToDevice),
-               "upload rungs");
+        P->ds_mode = std::getenv("RIPTIDE_AMD_PER_RUNG_LADDER")
+                         ? kLadderPerRung
+                         : ladder_split(prm.size, P->rungs, &P->rungs_f, &P->rungs_w);
+        for (const DsRung& d : P->rungs_w) P->ds_blocks_w += (uint32_t)((d.n + d.per_block - 1) / d.per_block);
+        auto upload = [](DsRung*& dst, const std::vector<DsRung>& src) {
+            ck(hipMalloc(&dst, std::max<size_t>(1, src.size()) * sizeof(DsRung)), "hipMalloc");
+            if (!src.empty())
+                ck(hipMemcpy(dst, src.data(), src.size() * sizeof(DsRung), hipMemcpyHostToDevice), "upload rungs");
+        };
+        upload(P->d_rungs, P->rungs);
+        if (P->ds_mode != kLadderPerRung) upload(P->d_rungs_f, P->rungs_f);
+        if (P->ds_mode == kLadderHybrid) upload(P->d_rungs_w, P->rungs_w);
     } catch (...) {
         delete P;
         throw;
@@ -735,20 +776,27 @@ void run_ladder(const rt_plan* P, const float* d_data, size_t batch, size_t data
         }
         ck(hipEventRecord(r.a, s), "hipEventRecord");
     }
-    if (P->ds_fused)
-        ck(launch_downsample_fused(d_data, P->pg.prm.size, data_stride, P->d_rungs, (uint32_t)P->rungs.size(),
-                                   ds_fused_margin(P->rungs.data(), P->rungs.size()), leaves, P->pg.leaf_floats,
+    if (P->ds_mode != kLadderPerRung)
+        ck(launch_downsample_fused(d_data, P->pg.prm.size, data_stride, P->d_rungs_f, (uint32_t)P->rungs_f.size(),
+                                   ds_fused_margin(P->rungs_f.data(), P->rungs_f.size()), leaves, P->pg.leaf_floats,
                                    (uint32_t)batch, s),
            "downsample_fused");
-    else
+    if (P->ds_mode == kLadderHybrid)
+        ck(launch_downsample_ladder(d_data, P->pg.prm.size, data_stride, P->d_rungs_w, (uint32_t)P->rungs_w.size(),
+                                    P->ds_blocks_w, leaves, P->pg.leaf_floats, (uint32_t)batch, s),
+           "downsample_ladder");
+    if (P->ds_mode == kLadderPerRung)
         ck(launch_downsample_ladder(d_data, P->pg.prm.size, data_stride, P->d_rungs, (uint32_t)P->rungs.size(),
                                     P->ds_blocks, leaves, P->pg.leaf_floats, (uint32_t)batch, s),
            "downsample_ladder");
     if (prof) {
         ck(hipEventRecord(r.b, s), "hipEventRecord");
-        double bytes = P->ds_fused ? 4.0 * P->pg.prm.size : 0.0;   // fused: the series is read once
-        for (const DsRung& d : P->rungs)
-            bytes += 4.0 * (double)d.n + (P->ds_fused ? 0.0 : (d.identity ? 4.0 * d.n : 4.0 * P->pg.prm.size));
+        // fused: the series is read once for its rungs; per-rung: once per rung
+        double bytes = P->ds_mode != kLadderPerRung ? 4.0 * P->pg.prm.size : 0.0;
+        for (const DsRung& d : P->rungs) {
+            const bool fused = P->ds_mode == kLadderFused || (P->ds_mode == kLadderHybrid && rung_fusable(d));
+            bytes += 4.0 * (double)d.n + (fused ? 0.0 : (d.identity ? 4.0 * d.n : 4.0 * P->pg.prm.size));
+        }
         r.alg = r.moved = bytes * batch;
         std::lock_guard<std::mutex> lk(g_prof.mu);
         g_prof.rec[1].push_back(r);
@@ -1240,7 +1288,7 @@ int rt_ladder_check(size_t size, double tsamp, double pmin, double pmax, size_t 
         PgramPlan pg;
         build_pgram_plan(prm, pg);
         const std::vector<DsRung> r = used_rungs(pg);
-        if (fused) *fused = ladder_fusable(size, r) ? 1 : 0;
+        if (fused) *fused = ladder_split(size, r, nullptr, nullptr);
         if (rungs) *rungs = r.size();
         return RT_OK;
     });

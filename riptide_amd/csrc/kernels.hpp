@@ -30,11 +30,15 @@ inline uint32_t ds_per_block(double f)
     return o > 256.0 ? 256u : (uint32_t)o;
 }
 
+// A block stages its span in LDS when that leaves it >= 32 outputs (f below
+// ~123); a wider rung's block of 256 outputs reads each window from global
+// memory (a staged block of 1-31 outputs left 225-255 of its threads idle
+// behind one span load: cfg5's long range, f up to ~1950).
 inline void ds_configure(DsRung& r)
 {
     const uint32_t o = r.identity ? 256u : ds_per_block(r.f);
-    r.staged = o != 0;
-    r.per_block = o ? o : 256u;
+    r.staged = o >= 32;
+    r.per_block = r.staged ? o : 256u;
 }
 
 // ffa_kernels.hip

@@ -512,13 +512,16 @@ def test_fused_ladder_matches_per_rung(monkeypatch):
 def test_fused_ladder_leaves_match_per_rung(monkeypatch):
     """The fused ladder's leaves themselves (every rung's downsampled series,
     the workspace's leaf buffer after plan.ladder) equal the per-rung kernel's
-    bit for bit: cfg2's full-size 57-rung ladder, the margin edge case and a
-    short odd-length series (the clipping tail block)."""
+    bit for bit: cfg2's full-size 57-rung ladder, the margin edge case, a
+    short odd-length series (the clipping tail block), cfg4, and cfg5's long
+    range (factors 30-1950: the rungs past the margin in the per-rung kernel
+    beside the fused one, rt_ladder_check = 2)."""
     import torch
     from riptide_amd import engine
     cases = [dict(n=1 << 23, tsamp=256e-6, pmin=0.1, pmax=10.0, bmin=240, bmax=260, ducy_max=0.2),
              inputs.LADDER_EDGE_CASE, dict(inputs.PGRAM_CASES[1], n=inputs.PGRAM_CASES[1]["n"] - 37),
-             inputs.PGRAM_CASES[3]]
+             inputs.PGRAM_CASES[3],
+             dict(n=1 << 21, tsamp=64e-6, pmin=2.0, pmax=120.0, bmin=960, bmax=1040, ducy_max=0.2)]
     for case in cases:
         x = torch.from_numpy(np.random.RandomState(11).normal(size=(2, case["n"])).astype(np.float32)).cuda()
         leaves = []

@@ -74,23 +74,26 @@ def test_ladder_path_choice(lib):
     assert r > 0
     # with the 512-float margin every BASELINE config and cfg5's
     # short / medium ranges still take the fused ladder (cfg4's largest factor
-    # is ~310); cfg5's long range (factors up to ~1800) takes the per-rung one
+    # is ~310); cfg5's long range (factors up to ~1950) takes the fused ladder
+    # for its rungs inside the margin and the per-rung kernel for the rest (2)
     cfg4 = dict(tsamp=64e-6, pmin=0.002, pmax=0.5, bmin=16, bmax=32)
     assert _ladder(lib, 1 << 22, cfg4)[0] == 1
     assert _ladder(lib, 2343750, dict(tsamp=256e-6, pmin=0.5, pmax=2.0, bmin=240, bmax=260))[0] == 1   # cfg1
     assert _ladder(lib, 1 << 22, dict(tsamp=256e-6, pmin=0.2, pmax=5.0, bmin=240, bmax=260))[0] == 1   # cfg3
     for rng in inputs.CFG5["ranges"]:
         s = rng["ffa_search"]
-        want = 0 if rng["name"] == "long" else 1
+        want = 2 if rng["name"] == "long" else 1
         assert _ladder(lib, inputs.CFG5["n"], dict(tsamp=inputs.CFG5["tsamp"], pmin=s["period_min"],
                                                    pmax=s["period_max"], bmin=s["bins_min"],
                                                    bmax=s["bins_max"]))[0] == want, rng["name"]
     # the margin's edge: largest factor with ceil(f) + 2 == 512 is fused,
-    # one more sample of window is not
+    # one more sample of window is not (that rung alone to the per-rung kernel)
     assert _ladder(lib, 1 << 20, inputs.LADDER_EDGE_CASE)[0] == 1
     over = dict(inputs.LADDER_EDGE_CASE, pmin=inputs.LADDER_EDGE_CASE["pmin"] * 510.5 / 509.5125)
     over["pmax"] = over["pmin"] * 1.125 ** 2 * 0.999
-    assert _ladder(lib, 1 << 20, over)[0] == 0
+    assert _ladder(lib, 1 << 20, over)[0] in (0, 2)
+    # every rung past the margin: nothing for the fused kernel
+    assert _ladder(lib, 1 << 22, dict(tsamp=64e-6, pmin=40.0, pmax=100.0, bmin=960, bmax=1040))[0] == 0
 
 
 def test_version(lib):
