@@ -6,7 +6,7 @@ the cone kernels' algorithmic bytes / HIP-event time against the 8 TB/s HBM
 peak.  The headline (cfg2 with dereddening) is bench.py's; this is the
 per-config table of DESIGN.md §5.
 
-usage (GPU box): python tools/bench_configs.py [batch]
+usage (GPU box): python tools/bench_configs.py [batch] [cfg5]
 """
 import json
 import os
@@ -22,13 +22,21 @@ CONFIGS = [
     dict(name="cfg3", n=1 << 22, tsamp=256e-6, pmin=0.2, pmax=5.0, bmin=240, bmax=260, ducy_max=0.2),
     dict(name="cfg4", n=1 << 22, tsamp=64e-6, pmin=0.002, pmax=0.5, bmin=16, bmax=32, ducy_max=0.2),
 ]
+# cfg5's three search ranges (riptide's example.yaml, tests/golden/inputs.py
+# CFG5) as periodograms alone: `python tools/bench_configs.py 16 cfg5`
+CONFIGS_CFG5 = [
+    dict(name="cfg5-short", n=1 << 23, tsamp=64e-6, pmin=0.2, pmax=0.5, bmin=240, bmax=260, ducy_max=0.2),
+    dict(name="cfg5-medium", n=1 << 23, tsamp=64e-6, pmin=0.5, pmax=2.0, bmin=480, bmax=520, ducy_max=0.2),
+    dict(name="cfg5-long", n=1 << 23, tsamp=64e-6, pmin=2.0, pmax=120.0, bmin=960, bmax=1040, ducy_max=0.2),
+]
 
 
 def main():
     import torch
     from riptide_amd import engine
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 16
-    for c in CONFIGS:
+    configs = CONFIGS_CFG5 if len(sys.argv) > 2 and sys.argv[2] == "cfg5" else CONFIGS
+    for c in configs:
         plan = engine.PeriodogramPlan.for_search(c["n"], c["tsamp"], c["pmin"], c["pmax"], c["bmin"], c["bmax"],
                                                  ducy_max=c["ducy_max"])
         x = torch.randn((B, c["n"]), device="cuda", dtype=torch.float32)
