@@ -14,6 +14,7 @@ per-rank peak lists -- tagged with their trial index -- are gathered once at
 the end (KB-scale, latency-bound) and put back in trial order.
 """
 import logging
+import os
 import typing
 
 import numpy as np
@@ -62,6 +63,7 @@ class EngineSearcher:
         self._plans = {}
         self._finders = {}
         self._ws = {}
+        self._side = {}
 
     def _plan(self, n, tsamp, conf):
         from . import engine
@@ -90,22 +92,57 @@ class EngineSearcher:
             self._ws[id(plan)] = ws
         return ws
 
+    def _side_stream(self, dev):
+        import torch
+        if dev not in self._side:
+            self._side[dev] = torch.cuda.Stream(device=dev)
+        return self._side[dev]
+
     def search_device(self, raw, tsamp, metadatas):
         """Peaks of every trial of a device batch raw [B, N] (float32): one
-        list per trial, in range order (WorkerPool.process_fname)."""
+        list per trial, in range order (WorkerPool.process_fname).
+
+        Every range's periodogram is queued first on the current stream;
+        each range's peak detection then runs on a side stream once its
+        periodogram is done (an event), so the detection's host stages (the
+        order statistics' polyfits, the selected rows' clustering) overlap
+        the later ranges' periodograms instead of leaving the GPU idle
+        between them.  Same kernels on the same data: same peaks."""
+        import torch
         from . import engine
         B, n = raw.shape
         ws = int(round(self.deredden_params["rmed_width"] / tsamp))
         x = engine.deredden_normalise(raw, ws, self.deredden_params["rmed_minpts"])
         out = [[] for _ in range(B)]
         dms = [m.get("dm") for m in metadatas]
+        main = torch.cuda.current_stream(x.device)
+        if os.environ.get("RIPTIDE_AMD_PEAKS_SERIAL"):
+            # A/B: each range's detection right after its periodogram, on
+            # the same stream (the GPU idles during the host stages)
+            for conf in self.range_confs:
+                plan = self._plan(n, tsamp, conf)
+                snr = plan.run(x, workspace=self._workspace(plan, B))
+                if self.check:
+                    plan.check()
+                for b, (peaks, _) in enumerate(self._finder(plan, n * tsamp, conf)(snr, dms=dms)):
+                    out[b].extend(peaks)
+            return out
+        runs = []
         for conf in self.range_confs:
             plan = self._plan(n, tsamp, conf)
             snr = plan.run(x, workspace=self._workspace(plan, B))
-            if self.check:
-                plan.check()          # device error flag: RuntimeError if a unit broke its budget
-            for b, (peaks, _) in enumerate(self._finder(plan, n * tsamp, conf)(snr, dms=dms)):
+            ev = torch.cuda.Event()
+            ev.record(main)
+            runs.append((conf, plan, snr, ev))
+        side = self._side_stream(x.device)
+        for conf, plan, snr, ev in runs:
+            side.wait_event(ev)
+            snr.record_stream(side)
+            for b, (peaks, _) in enumerate(self._finder(plan, n * tsamp, conf)(snr, dms=dms, stream=side)):
                 out[b].extend(peaks)
+        if self.check:
+            for _, plan, _, _ in runs:
+                plan.check()          # device error flag: RuntimeError if a unit broke its budget
         return out
 
     def search_samples(self, samples, tsamps, metadatas):
