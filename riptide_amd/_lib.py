@@ -98,6 +98,15 @@ def load():
         raise ImportError(
             f"riptide_amd engine library not found at {LIB_PATH}; build it with "
             "`make -C riptide_amd/csrc` or `python -c 'import __graft_entry__ as g; g.build()'`")
+    # One HIP runtime per process: torch ships its own libamdhip64, and an
+    # engine library loaded before torch binds /opt/rocm's instead -- the
+    # engine's launches then fail with "no ROCm-capable device is detected"
+    # once torch initialises its runtime (`import riptide_amd; import torch`).
+    # Importing torch first makes the engine resolve to torch's runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     # The plan pointer is opaque: rt_plan_create takes an rt_plan** (void*)
     lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
     for name, (res, args) in _SIGNATURES.items():

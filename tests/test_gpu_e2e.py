@@ -396,3 +396,16 @@ def test_two_host_threads_one_device():
     prof = engine.profile_read(0)
     assert prof["launches"] == 2 * 3 * per_run
     plan.check()
+
+
+def test_engine_imported_before_torch():
+    """`import riptide_amd` before `import torch` (a fresh process): the engine
+    library binds torch's HIP runtime (riptide_amd/_lib.py load imports torch
+    first); loaded alone it bound /opt/rocm's and its launches failed with "no
+    ROCm-capable device is detected" once torch initialised its own."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(repo, "tools", "import_order_check.py")],
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0 and "import order ok" in r.stdout, r.stdout + r.stderr

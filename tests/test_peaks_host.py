@@ -82,3 +82,25 @@ def test_cluster_peaks_pipeline_order():
     got = sorted(sorted(p.ip for p in cl) for cl in clusters)
     assert got == [[0, 1, 2, 3], [4, 5], [6], [7], [8, 9]]
     assert cluster_peaks([], rad, tobs) == ([], [])
+
+
+def test_polyfit_columns_bit_exact():
+    """peaks.polyfit_columns / poly1d_coefficients == np.poly1d(np.polyfit(x,
+    y, deg)).coefficients for every row, bit for bit (the threshold polynomial
+    of find_peaks, peak_detection.py:187-199): segment counts of the
+    BASELINE / cfg5 ranges, float32 and float64 rows, exact-zero leading
+    coefficients (a constant and a linear row)."""
+    from riptide_amd.peaks import poly1d_coefficients, polyfit_columns
+    rng = np.random.default_rng(5)
+    for nseg in (10, 11, 53, 97, 400):
+        x = np.log(np.sort(rng.uniform(0.008, 12.0, nseg)))
+        for dtype in (np.float64, np.float32):
+            Y = rng.normal(7.0, 0.6, (37, nseg)).astype(dtype)
+            Y[0] = 6.5                                   # constant: leading coefficients ~0
+            Y[1] = (2.0 * x + 1.0).astype(dtype)         # linear
+            got = polyfit_columns(x, Y, 2)
+            for k in range(Y.shape[0]):
+                want = np.poly1d(np.polyfit(x, Y[k], 2)).coefficients
+                assert np.array_equal(poly1d_coefficients(got[k]), want), (nseg, dtype, k)
+    assert np.array_equal(poly1d_coefficients([0.0, 0.0, 3.0]), np.poly1d([0.0, 0.0, 3.0]).coefficients)
+    assert np.array_equal(poly1d_coefficients([0.0]), np.poly1d([0.0]).coefficients)
