@@ -100,33 +100,22 @@ class EngineSearcher:
 
     def search_device(self, raw, tsamp, metadatas):
         """Peaks of every trial of a device batch raw [B, N] (float32): one
-        list per trial, in range order (WorkerPool.process_fname).
+        list per trial, in range order (WorkerPool.process_fname)."""
+        return self._detect(self._enqueue(raw, tsamp, metadatas))
 
-        Every range's periodogram is queued first on the current stream;
-        each range's peak detection then runs on a side stream once its
-        periodogram is done (an event), so the detection's host stages (the
-        order statistics' polyfits, the selected rows' clustering) overlap
-        the later ranges' periodograms instead of leaving the GPU idle
-        between them.  Same kernels on the same data: same peaks."""
+    def _enqueue(self, raw, tsamp, metadatas):
+        """Queue a device batch's deredden + normalise and every range's
+        periodogram on the current stream; returns the pending batch for
+        _detect.  Nothing here waits for the device."""
         import torch
         from . import engine
         B, n = raw.shape
         ws = int(round(self.deredden_params["rmed_width"] / tsamp))
         x = engine.deredden_normalise(raw, ws, self.deredden_params["rmed_minpts"])
-        out = [[] for _ in range(B)]
         dms = [m.get("dm") for m in metadatas]
         main = torch.cuda.current_stream(x.device)
         if os.environ.get("RIPTIDE_AMD_PEAKS_SERIAL"):
-            # A/B: each range's detection right after its periodogram, on
-            # the same stream (the GPU idles during the host stages)
-            for conf in self.range_confs:
-                plan = self._plan(n, tsamp, conf)
-                snr = plan.run(x, workspace=self._workspace(plan, B))
-                if self.check:
-                    plan.check()
-                for b, (peaks, _) in enumerate(self._finder(plan, n * tsamp, conf)(snr, dms=dms)):
-                    out[b].extend(peaks)
-            return out
+            return {"serial": True, "x": x, "n": n, "tsamp": tsamp, "dms": dms}
         runs = []
         for conf in self.range_confs:
             plan = self._plan(n, tsamp, conf)
@@ -134,30 +123,92 @@ class EngineSearcher:
             ev = torch.cuda.Event()
             ev.record(main)
             runs.append((conf, plan, snr, ev))
-        side = self._side_stream(x.device)
-        for conf, plan, snr, ev in runs:
+        return {"serial": False, "runs": runs, "n": n, "tsamp": tsamp, "dms": dms, "B": B, "device": x.device}
+
+    def _detect(self, pend):
+        """Peak detection of a pending batch, range by range, on a side
+        stream: each range's detection starts once its periodogram is done
+        (an event), so its host stages (the order statistics' polyfits, the
+        selected rows' clustering) overlap the periodograms queued after it
+        -- the later ranges', and with submit_samples the next batch's --
+        instead of leaving the GPU idle.  Same kernels on the same data:
+        same peaks."""
+        n, tsamp, dms = pend["n"], pend["tsamp"], pend["dms"]
+        if pend["serial"]:
+            # A/B (RIPTIDE_AMD_PEAKS_SERIAL): each range's detection right
+            # after its periodogram, on the same stream, nothing queued ahead
+            x = pend["x"]
+            out = [[] for _ in range(x.shape[0])]
+            for conf in self.range_confs:
+                plan = self._plan(n, tsamp, conf)
+                snr = plan.run(x, workspace=self._workspace(plan, x.shape[0]))
+                if self.check:
+                    plan.check()
+                for b, (peaks, _) in enumerate(self._finder(plan, n * tsamp, conf)(snr, dms=dms)):
+                    out[b].extend(peaks)
+            return out
+        out = [[] for _ in range(pend["B"])]
+        side = self._side_stream(pend["device"])
+        for conf, plan, snr, ev in pend["runs"]:
             side.wait_event(ev)
             snr.record_stream(side)
             for b, (peaks, _) in enumerate(self._finder(plan, n * tsamp, conf)(snr, dms=dms, stream=side)):
                 out[b].extend(peaks)
         if self.check:
-            for _, plan, _, _ in runs:
-                plan.check()          # device error flag: RuntimeError if a unit broke its budget
+            for _, plan, _, _ in pend["runs"]:
+                # device error flag, read on the side stream: ordered after
+                # this batch's periodograms (the events), not waiting for
+                # what is queued behind them; RuntimeError if a unit broke
+                # its budget
+                plan.check(side)
         return out
+
+    def submit_samples(self, samples, tsamps, metadatas, uploaded=None):
+        """search_samples in two halves: uploads and periodograms of every
+        device batch queued now, peak detection when the returned callable is
+        called (-> per-trial peak lists in input order).  A caller that
+        submits chunk k + 1 before collecting chunk k keeps the device busy
+        through chunk k's host stages (GpuWorkerPool.search_chunks); device
+        batches within one call are pipelined the same way.  `uploaded()`, if
+        given, is called once the last batch's upload is queued: the host
+        samples may be reused after the device work queued at that moment (an
+        event)."""
+        from .reading import upload_samples
+        batches = []
+        for (n, tsamp), idx in _group_by_shape(samples, tsamps).items():
+            for b0 in range(0, len(idx), self.batch):
+                batches.append((tsamp, idx[b0:b0 + self.batch]))
+        per = [None] * len(samples)
+        state = {"next": 0, "pending": []}
+
+        def enqueue_one():
+            k = state["next"]
+            if k < len(batches):
+                tsamp, chunk = batches[k]
+                x = upload_samples([samples[i] for i in chunk], device=self.device)
+                if k + 1 == len(batches) and uploaded is not None:
+                    uploaded()
+                state["pending"].append((chunk, self._enqueue(x, tsamp, [metadatas[i] for i in chunk])))
+                state["next"] = k + 1
+
+        def collect():
+            while state["pending"]:
+                enqueue_one()           # batch j + 1 queued before batch j's detection
+                chunk, pend = state["pending"].pop(0)
+                for i, peaks in zip(chunk, self._detect(pend)):
+                    per[i] = peaks
+            return per
+
+        enqueue_one()
+        if not batches and uploaded is not None:
+            uploaded()
+        return collect
 
     def search_samples(self, samples, tsamps, metadatas):
         """Per-trial peak lists of host sample arrays (float32 or 8-bit, as
         stored): grouped by (length, tsamp), uploaded in device batches
         (8-bit data converted on the device), results in input order."""
-        from .reading import upload_samples
-        per = [None] * len(samples)
-        for (n, tsamp), idx in _group_by_shape(samples, tsamps).items():
-            for b0 in range(0, len(idx), self.batch):
-                chunk = idx[b0:b0 + self.batch]
-                x = upload_samples([samples[i] for i in chunk], device=self.device)
-                for i, peaks in zip(chunk, self.search_device(x, tsamp, [metadatas[i] for i in chunk])):
-                    per[i] = peaks
-        return per
+        return self.submit_samples(samples, tsamps, metadatas)()
 
     def __call__(self, trials):
         return self.search_samples([t.data for t in trials], [t.tsamp for t in trials],

@@ -84,6 +84,21 @@ def poly1d_coefficients(c):
     return c if c.size else np.array([0.0])
 
 
+def poly1d_table(fits):
+    """poly1d_coefficients of every fit in a [B, W, deg + 1] array at once:
+    (the kernel's coefficient table -- leading zeros of either sign, as
+    np.trim_zeros sees them, stored as +0, and 0 * x + c = c keeps
+    np.polyval's value exactly -- and the reference's polyco of every
+    (trial, width), [0.] for an all-zero fit)."""
+    B, W, n = fits.shape
+    lead = np.logical_and.accumulate(fits == 0, axis=-1)
+    first = lead.sum(axis=-1)
+    coeffs = np.where(lead, 0.0, fits)
+    polycos = [[fits[b, iw, first[b, iw]:] if first[b, iw] < n else np.array([0.0])
+                for iw in range(W)] for b in range(B)]
+    return coeffs, polycos
+
+
 def percentiles_from_order_stats(stats, gamma):
     """(s25, smed, s75) float64 arrays from the [..., 6] order statistics."""
     x = np.asarray(stats, dtype=np.float64)
@@ -135,21 +150,12 @@ class PeakFinder:
         sstd = (s75 - s25) / 1.349
         sc = smed + self.nstd * sstd
         B, W = sc.shape[0], sc.shape[1]
-        coeffs = np.zeros((B, W, max(self.ncoef, 1)), dtype=np.float64)
-        polycos = [[None] * W for _ in range(B)]
-        fits = (polyfit_columns(self.logfc, sc.reshape(B * W, -1), self.polydeg).reshape(B, W, -1)
-                if len(self.fc) >= self.minseg else None)
-        for b in range(B):
-            for iw in range(W):
-                if fits is not None:
-                    polyco = poly1d_coefficients(fits[b, iw])     # np.poly1d(np.polyfit(...)).coefficients
-                else:
-                    polyco = [self.smin]
-                c = np.asarray(poly1d_coefficients(polyco), dtype=np.float64)
-                # leading zeros keep np.polyval's value exactly (0 * x + c = c)
-                coeffs[b, iw, coeffs.shape[2] - c.size:] = c
-                polycos[b][iw] = polyco
-        return coeffs, polycos
+        if len(self.fc) < self.minseg:
+            coeffs = np.zeros((B, W, 1), dtype=np.float64)
+            coeffs[..., 0] = poly1d_coefficients([self.smin])[-1]
+            return coeffs, [[[self.smin] for _ in range(W)] for _ in range(B)]
+        fits = polyfit_columns(self.logfc, sc.reshape(B * W, -1), self.polydeg).reshape(B, W, -1)
+        return poly1d_table(fits)
 
     def __call__(self, snr, dms=None, stream=None):
         """Peaks of every trial: list of (peaks sorted by S/N, polycos).

@@ -14,10 +14,11 @@ file, in range order -- the order WorkerPool.process_fname_list returns them
 in.
 
 Long file lists (a rank's share of a beam, dmiter.py:231-243 chunks) go
-through `search_chunks`: a reader thread reads chunk k + 1 into one half of a
-fixed ring of page-locked slots while chunk k is searched from the other
-half, so host memory stays at 2 x chunk files whatever the list length and
-file reads overlap the device work.
+through `search_chunks`: a reader thread reads chunk k + 1 into one part of a
+fixed three-part ring of page-locked slots while chunk k is on the device and
+chunk k - 1's peaks are detected, so host memory stays at 3 x chunk files
+whatever the list length, and file reads and host detection stages overlap
+the device work.
 """
 import logging
 import threading
@@ -29,6 +30,10 @@ log = logging.getLogger("riptide.worker_pool")
 
 # host threads reading a chunk's files
 _READ_THREADS = 8
+
+# page-locked ring parts of search_chunks: chunk k - 1 detecting, chunk k on
+# the device, chunk k + 1 being read
+_RING_PARTS = 3
 
 
 def iterate_chunks(fnames, chunksize=1):
@@ -62,12 +67,12 @@ class GpuWorkerPool:
         self.device = device
         self.searcher = EngineSearcher(self.deredden_params, self.range_confs, device=device, batch=self.batch)
         self._pinned = {}
-        # per ring half: a device event recorded after the half's samples were
-        # last consumed; a half is refilled only after its event completed
-        self._half_done = {}
+        # per ring part: a device event recorded after the part's samples were
+        # last uploaded; a part is refilled only after its event completed
+        self._part_done = {}
 
     def _stager(self, slot):
-        """staging(nbytes) for ring slot `slot` = (half, file index): a page-locked uint8 buffer,
+        """staging(nbytes) for ring slot `slot` = (part, file index): a page-locked uint8 buffer,
         grown when a file needs more (None without a GPU or for PRESTO)."""
         import torch
         if self.fmt != "sigproc" or not torch.cuda.is_available():
@@ -81,14 +86,14 @@ class GpuWorkerPool:
             return buf.numpy()
         return staging
 
-    def _wait_half(self, half):
-        ev = self._half_done.pop(half, None)
+    def _wait_part(self, part):
+        ev = self._part_done.pop(part, None)
         if ev is not None:
             ev.synchronize()
 
-    def _release_half(self, half):
-        """Record that the device work reading ring half `half` is queued:
-        the next fill of the half waits for it (search_samples happens to
+    def _release_part(self, part):
+        """Record that the device work reading ring part `part` is queued:
+        the next fill of the part waits for it (search_samples happens to
         synchronise when its peaks reach the host; this does not rely on it)."""
         import torch
         if not torch.cuda.is_available():
@@ -96,13 +101,13 @@ class GpuWorkerPool:
         dev = torch.device("cuda", torch.cuda.current_device() if self.device is None else self.device)
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(dev))
-        self._half_done[half] = ev
+        self._part_done[part] = ev
 
-    def _read(self, fnames, half):
+    def _read(self, fnames, part):
         """Read a chunk's files (concurrently: np.fromfile / readinto release
-        the GIL) into ring half `half`.  Returns (raws, metas, tsamps)."""
-        self._wait_half(half)
-        stagers = [self._stager((half, i)) for i in range(len(fnames))]
+        the GIL) into ring part `part`.  Returns (raws, metas, tsamps)."""
+        self._wait_part(part)
+        stagers = [self._stager((part, i)) for i in range(len(fnames))]
         if len(fnames) > 1:
             from concurrent.futures import ThreadPoolExecutor
             with ThreadPoolExecutor(max_workers=min(len(fnames), _READ_THREADS)) as ex:
@@ -111,15 +116,36 @@ class GpuWorkerPool:
             loaded = [_raw_samples(fn, self.fmt, staging=st) for fn, st in zip(fnames, stagers)]
         return [t[0] for t in loaded], [t[1] for t in loaded], [t[2] for t in loaded]
 
-    def _search(self, loaded, half):
+    def _search(self, loaded, part):
+        return self._submit(loaded, part)()
+
+    def _submit(self, loaded, part):
+        """Queue a chunk's uploads and periodograms; returns the callable that
+        runs its peak detection (-> per-file peak lists).  The ring part is
+        released (its event) once the chunk's last upload is queued."""
         raws, metas, tsamps = loaded
+        released = []
+
+        def uploaded():
+            self._release_part(part)
+            released.append(True)
+        collect = None
         try:
-            per_file = self.searcher.search_samples(raws, tsamps, metas)
+            collect = self.searcher.submit_samples(raws, tsamps, metas, uploaded=uploaded)
         finally:
-            self._release_half(half)
-        for meta, peaks in zip(metas, per_file):
-            log.debug(f"Done searching DM = {meta.get('dm')}, peaks found: {len(peaks)}")
-        return per_file
+            if collect is None and not released:
+                self._release_part(part)
+
+        def finish():
+            try:
+                per_file = collect()
+            finally:
+                if not released:
+                    self._release_part(part)
+            for meta, peaks in zip(metas, per_file):
+                log.debug(f"Done searching DM = {meta.get('dm')}, peaks found: {len(peaks)}")
+            return per_file
+        return finish
 
     def process_fname(self, fname):
         return self.process_fname_list([fname])
@@ -134,8 +160,12 @@ class GpuWorkerPool:
         """Search a long file list chunk by chunk (DMIterator chunks of
         `chunksize`, default `batch`), yielding (first index, per-file peak
         lists) per chunk in order.  Chunk k + 1 is read by a background
-        thread into the other half of the page-locked ring while chunk k is
-        on the device; at most two chunks of samples are held at any time."""
+        thread into a free part of the page-locked ring while chunk k's
+        periodograms are queued and chunk k - 1's peak detection runs, so
+        the device works through the detection's host stages
+        (EngineSearcher.submit_samples): three ring parts (k - 1 detecting,
+        k on the device, k + 1 being read), at most three chunks of samples
+        held whatever the list length."""
         fnames = list(fnames)
         cs = int(chunksize or self.batch)
         chunks = [(i, fnames[i:i + cs]) for i in range(0, len(fnames), cs)]
@@ -145,12 +175,13 @@ class GpuWorkerPool:
 
         def reader(k):
             try:
-                box[k] = self._read(chunks[k][1], k % 2)
+                box[k] = self._read(chunks[k][1], k % _RING_PARTS)
             except BaseException as e:   # re-raised in the searching thread
                 box[k] = e
 
         th = threading.Thread(target=reader, args=(0,), daemon=True)
         th.start()
+        prev = None
         try:
             for k, (first, _) in enumerate(chunks):
                 th.join()
@@ -158,10 +189,16 @@ class GpuWorkerPool:
                 if isinstance(loaded, BaseException):
                     raise loaded
                 if k + 1 < len(chunks):
-                    # the next chunk's half was last read by chunk k - 1,
-                    # whose device event _read waits for before refilling it
+                    # the next chunk's part was last read by chunk k - 2,
+                    # collected in the previous iteration: its uploads are
+                    # queued, and _read waits for their event before refilling
                     th = threading.Thread(target=reader, args=(k + 1,), daemon=True)
                     th.start()
-                yield first, self._search(loaded, k % 2)
+                cur = (first, self._submit(loaded, k % _RING_PARTS))
+                if prev is not None:
+                    yield prev[0], prev[1]()      # chunk k - 1's detection while chunk k is on the device
+                prev = cur
+            if prev is not None:
+                yield prev[0], prev[1]()
         finally:
             th.join()      # no reader left writing into the ring

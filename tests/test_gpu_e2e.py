@@ -298,6 +298,33 @@ def test_worker_pool_mixed_shapes_matches_per_file(e2e, tmp_path):
     assert [p.snr for p in got] == [p.snr for p in ref]          # same kernels: identical
 
 
+def test_search_chunks_pipelined_matches_per_file(e2e, tmp_path):
+    """GpuWorkerPool.search_chunks with chunk k's periodograms queued before
+    chunk k - 1's peak detection (three-part page-locked ring, detection on a
+    side stream): chunks mixing two lengths and an 8-bit file, a batch that
+    splits them (batches pipelined within a chunk too), a short last chunk --
+    the per-chunk peak lists equal searching every file on its own."""
+    from riptide_amd.reading import write_sigproc
+    from riptide_amd.worker_pool import GpuWorkerPool
+    c = inputs.CFG5
+    fns = []
+    for j, k in enumerate((5, 2, 7, 3, 4, 6, 1, 0, 2, 6, 5)):
+        n = (1 << 20) if j % 3 == 1 else (3 << 19)
+        data, hdr = inputs.cfg5_trial(k, n=n)
+        fn = str(tmp_path / f"pipe_{j}.tim")
+        write_sigproc(fn, data, hdr)
+        fns.append(fn)
+    pool = GpuWorkerPool(c["dereddening"], c["ranges"][:2], fmt="sigproc", batch=2)
+    chunks = list(pool.search_chunks(fns, chunksize=3))
+    assert [first for first, _ in chunks] == [0, 3, 6, 9]
+    got = [p for _, per_file in chunks for plist in per_file for p in plist]
+    one = GpuWorkerPool(c["dereddening"], c["ranges"][:2], fmt="sigproc", batch=1)
+    ref = [p for fn in fns for p in one.process_fname(fn)]
+    assert len(got) == len(ref) > 0
+    assert [(p.dm, p.ip, p.iw) for p in got] == [(p.dm, p.ip, p.iw) for p in ref]
+    assert [p.snr for p in got] == [p.snr for p in ref]
+
+
 # ---------------------------------------------------------------- C ABI robustness
 _ERROR_FLAG_BODY = r"""
 import sys

@@ -104,3 +104,27 @@ def test_polyfit_columns_bit_exact():
                 assert np.array_equal(poly1d_coefficients(got[k]), want), (nseg, dtype, k)
     assert np.array_equal(poly1d_coefficients([0.0, 0.0, 3.0]), np.poly1d([0.0, 0.0, 3.0]).coefficients)
     assert np.array_equal(poly1d_coefficients([0.0]), np.poly1d([0.0]).coefficients)
+
+
+def test_poly1d_table_matches_per_fit():
+    """peaks.poly1d_table (every (trial, width) at once) == the per-fit
+    np.poly1d coefficients and their right-aligned, zero-padded table rows,
+    including leading zeros of both signs and all-zero fits."""
+    from riptide_amd.peaks import poly1d_coefficients, poly1d_table
+    rng = np.random.default_rng(11)
+    fits = rng.normal(0.0, 1.0, (5, 7, 3))
+    fits[0, 0] = [0.0, 0.0, 4.0]
+    fits[0, 1] = [-0.0, 2.0, 1.0]
+    fits[0, 2] = [0.0, -0.0, 0.0]
+    fits[1, 3] = [0.0, 0.0, -0.0]
+    fits[2, 4] = [1.0, 0.0, 0.0]
+    fits[3, 5] = [-0.0, 0.0, 5.0]
+    coeffs, polycos = poly1d_table(fits)
+    for b in range(fits.shape[0]):
+        for iw in range(fits.shape[1]):
+            want = np.poly1d(fits[b, iw]).coefficients
+            assert np.array_equal(polycos[b][iw], want) and polycos[b][iw].dtype == want.dtype
+            row = np.zeros(3)
+            c = poly1d_coefficients(want)
+            row[3 - c.size:] = c
+            assert np.array_equal(coeffs[b, iw], row) and not np.signbit(coeffs[b, iw][:3 - c.size]).any()
