@@ -30,29 +30,24 @@ struct SegRanks {           // ranks of the order statistics, passed by value
     uint32_t r[kMaxSegmentRanks];
 };
 
-// One block per (segment, width, trial); the segment padded to n2 (a power
-// of two) in dynamic LDS: 256 threads up to 4096 points, 1024 beyond (up to
-// kMaxSegmentPoints = 32768, 128 KiB).
+// One block per (segment, width, trial).  The requested order statistics
+// are selected, not sorted for: the segment's values (dynamic LDS, n2 =
+// per_seg rounded up to a power of two) are binned by value between their
+// minimum and maximum into nb = min(n2, kSelBins) bins -- (x - min) * scale
+// truncated is monotone in x, so every value of a lower bin is smaller than
+// every value of a higher one -- the bins' counts prefix-summed, and each
+// rank found in its bin's few values (a counting select among them).  About
+// five passes over the segment instead of the log2(n2)^2 / 2 compare-exchange
+// stages of a bitonic sort.  The bitonic sort (+inf padded) stays as the
+// fallback for segments the binning cannot split: a NaN-free segment with an
+// infinite value, a single distinct value, or more than cap values in a
+// selected bin (a far outlier crowding the rest into few bins).
+constexpr int kSelBins = 4096;
+constexpr int kSelLists = kMaxSegmentRanks;
+
 template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void segment_order_stats_kernel(
-    const float* __restrict__ snrs, uint64_t snr_stride, uint32_t W, uint32_t per_seg, uint32_t n2,
-    SegRanks ranks, uint32_t nranks, float* __restrict__ out)
+__device__ void bitonic_ascending(float* key, uint32_t n2)
 {
-    extern __shared__ __attribute__((aligned(16))) float key[];
-    const uint32_t seg = blockIdx.x, iw = blockIdx.y, trial = blockIdx.z;
-    const uint32_t nseg = gridDim.x;
-    const float* s = snrs + (uint64_t)trial * snr_stride + (uint64_t)seg * per_seg * W + iw;
-    int nan_seen = 0;
-    for (uint32_t i = threadIdx.x; i < n2; i += BLOCK) {
-        float v = INFINITY;
-        if (i < per_seg) {
-            v = s[(uint64_t)i * W];
-            nan_seen |= v != v;
-        }
-        key[i] = v;
-    }
-    const int has_nan = __syncthreads_or(nan_seen);
-    // bitonic sort, ascending
     for (uint32_t k = 2; k <= n2; k <<= 1) {
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
             for (uint32_t i = threadIdx.x; i < n2; i += BLOCK) {
@@ -69,8 +64,156 @@ __global__ __launch_bounds__(BLOCK) void segment_order_stats_kernel(
             __syncthreads();
         }
     }
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void segment_order_stats_kernel(
+    const float* __restrict__ snrs, uint64_t snr_stride, uint32_t W, uint32_t per_seg, uint32_t n2,
+    SegRanks ranks, uint32_t nranks, float* __restrict__ out)
+{
+    constexpr int kWaves = BLOCK / 64;
+    extern __shared__ __attribute__((aligned(16))) float key[];        // n2 values, then nb bins
+    __shared__ float wmin[kWaves], wmax[kWaves];
+    __shared__ uint32_t wsum[kWaves];
+    __shared__ uint32_t tbin[kSelLists], tbase[kSelLists], lid[kSelLists], lcnt[kSelLists], win[kSelLists];
+    const uint32_t seg = blockIdx.x, iw = blockIdx.y, trial = blockIdx.z;
+    const uint32_t nseg = gridDim.x;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const float* s = snrs + (uint64_t)trial * snr_stride + (uint64_t)seg * per_seg * W + iw;
     float* o = out + (((uint64_t)trial * W + iw) * nseg + seg) * nranks;
-    if (threadIdx.x < nranks) o[threadIdx.x] = has_nan ? NAN : key[ranks.r[threadIdx.x]];
+    uint32_t* hist = reinterpret_cast<uint32_t*>(key + n2);
+    const uint32_t nb = n2 < (uint32_t)kSelBins ? n2 : (uint32_t)kSelBins;
+    int nan_seen = 0;
+    float mn = INFINITY, mx = -INFINITY;
+    for (uint32_t i = tid; i < n2; i += BLOCK) {
+        float v = INFINITY;
+        if (i < per_seg) {
+            v = s[(uint64_t)i * W];
+            nan_seen |= v != v;
+            mn = fminf(mn, v);
+            mx = fmaxf(mx, v);
+        }
+        key[i] = v;
+    }
+    for (uint32_t i = tid; i < nb; i += BLOCK) hist[i] = 0u;
+    for (int d = 32; d >= 1; d >>= 1) {
+        mn = fminf(mn, __shfl_xor(mn, d));
+        mx = fmaxf(mx, __shfl_xor(mx, d));
+    }
+    if (lane == 0) {
+        wmin[wave] = mn;
+        wmax[wave] = mx;
+    }
+    const int has_nan = __syncthreads_or(nan_seen);
+    if (has_nan) {
+        if (tid < nranks) o[tid] = NAN;
+        return;
+    }
+    mn = wmin[0];
+    mx = wmax[0];
+#pragma unroll
+    for (int w = 1; w < kWaves; ++w) {
+        mn = fminf(mn, wmin[w]);
+        mx = fmaxf(mx, wmax[w]);
+    }
+    const float scale = (float)nb / (mx - mn);
+    // block-uniform: the binning splits the segment (finite, distinct values)
+    bool binned = per_seg > 64 && mn > -INFINITY && mx < INFINITY && mx > mn && scale > 0.f && scale < 3.0e38f;
+    if (binned) {
+        for (uint32_t i = tid; i < per_seg; i += BLOCK) {
+            const uint32_t b = min((uint32_t)((key[i] - mn) * scale), nb - 1u);
+            atomicAdd(&hist[b], 1u);
+        }
+        __syncthreads();
+        // exclusive prefix sum of the bins: a thread's run of consecutive
+        // bins, then the runs' totals scanned across the block
+        const uint32_t per = (nb + BLOCK - 1) / BLOCK;
+        const uint32_t b0 = min(tid * per, nb), b1 = min(b0 + per, nb);
+        uint32_t run = 0;
+        for (uint32_t b = b0; b < b1; ++b) run += hist[b];
+        uint32_t incl = run;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d);
+            if ((int)lane >= d) incl += y;
+        }
+        if (lane == 63) wsum[wave] = incl;
+        if (tid < kSelLists) {
+            lcnt[tid] = 0u;
+            win[tid] = 0xFFFFFFFFu;
+            tbin[tid] = 0xFFFFFFFFu;
+        }
+        __syncthreads();
+        uint32_t base = incl - run;
+        for (int w = 0; w < (int)wave; ++w) base += wsum[w];
+        // the bin of every rank: cum[b] <= r < cum[b] + count[b]
+        for (uint32_t b = b0; b < b1; ++b) {
+            const uint32_t c = hist[b];
+            for (uint32_t q = 0; q < nranks; ++q) {
+                const uint32_t r = ranks.r[q];
+                if (r >= base && r < base + c) {
+                    tbin[q] = b;
+                    tbase[q] = base;
+                }
+            }
+            base += c;
+        }
+        __syncthreads();
+        int unset = 0;      // a rank past the segment (the bitonic path's +inf padding)
+        for (uint32_t q = 0; q < nranks; ++q) unset |= tbin[q] == 0xFFFFFFFFu;
+        if (tid == 0) {
+            for (uint32_t q = 0; q < nranks; ++q) {
+                uint32_t l = q;
+                for (uint32_t e = 0; e < q; ++e)
+                    if (tbin[e] == tbin[q]) {
+                        l = lid[e];
+                        break;
+                    }
+                lid[q] = l;
+            }
+        }
+        __syncthreads();
+        // the selected bins' values, one list per distinct bin, in the bin area
+        const uint32_t cap = nb / (uint32_t)kSelLists;
+        for (uint32_t i = tid; i < per_seg; i += BLOCK) {
+            const float v = key[i];
+            const uint32_t b = min((uint32_t)((v - mn) * scale), nb - 1u);
+            for (uint32_t q = 0; q < nranks; ++q) {
+                if (lid[q] == q && b == tbin[q]) {
+                    const uint32_t pos = atomicAdd(&lcnt[q], 1u);
+                    if (pos < cap) reinterpret_cast<float*>(hist)[q * cap + pos] = v;
+                }
+            }
+        }
+        __syncthreads();
+        int over = unset;
+        for (uint32_t q = 0; q < nranks && !unset; ++q) over |= lcnt[lid[q]] > cap;
+        binned = !over;
+        if (binned) {
+            // rank r - cum[bin] within its bin's list: the value with that
+            // many smaller ones (ties: the lowest list position)
+            const float* lists = reinterpret_cast<const float*>(hist);
+            for (uint32_t q = 0; q < nranks; ++q) {
+                const uint32_t l = lid[q], m = lcnt[l], k = ranks.r[q] - tbase[q];
+                const float* L = lists + l * cap;
+                for (uint32_t t = tid; t < m; t += BLOCK) {
+                    const float e = L[t];
+                    uint32_t lt = 0, eq = 0;
+                    for (uint32_t j = 0; j < m; ++j) {
+                        lt += L[j] < e;
+                        eq += L[j] == e;
+                    }
+                    if (lt <= k && k < lt + eq) atomicMin(&win[q], t);
+                }
+            }
+            __syncthreads();
+            if (tid < nranks) o[tid] = lists[lid[tid] * cap + win[tid]];
+            return;
+        }
+    }
+    // fallback: bitonic sort of the padded segment, ascending
+    __syncthreads();
+    bitonic_ascending<BLOCK>(key, n2);
+    if (tid < nranks) o[tid] = key[ranks.r[tid]];
 }
 
 __global__ __launch_bounds__(kPeakBlock) void threshold_select_kernel(
@@ -103,7 +246,7 @@ hipError_t launch_segment_order_stats(const float* snrs, uint64_t snr_stride, ui
     for (uint32_t i = 0; i < nranks; ++i) rk.r[i] = ranks[i];
     uint32_t n2 = 1;
     while (n2 < per_seg) n2 <<= 1;
-    const size_t lds = (size_t)n2 * sizeof(float);
+    const size_t lds = ((size_t)n2 + (n2 < (uint32_t)kSelBins ? n2 : (uint32_t)kSelBins)) * sizeof(float);
     if (n2 <= 4096) {
         hipLaunchKernelGGL(segment_order_stats_kernel<kPeakBlock>, dim3(nseg, W, batch), dim3(kPeakBlock), lds, s,
                            snrs, snr_stride, W, per_seg, n2, rk, nranks, out);
@@ -120,7 +263,7 @@ hipError_t launch_segment_order_stats(const float* snrs, uint64_t snr_stride, ui
             if (dev >= 64 || !(done >> dev & 1)) {
                 e = hipFuncSetAttribute(reinterpret_cast<const void*>(segment_order_stats_kernel<1024>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)(kMaxSegmentPoints * sizeof(float)));
+                                        (int)((kMaxSegmentPoints + kSelBins) * sizeof(float)));
                 if (e != hipSuccess) return e;
                 if (dev < 64) done |= 1ull << dev;
             }

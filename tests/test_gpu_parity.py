@@ -808,6 +808,62 @@ def test_segment_order_stats_long_segments(rt, per_seg):
                     assert np.array_equal(got[b, iw, sg], np.sort(col)[ranks])
 
 
+@pytest.mark.parametrize("kind", ["rounded", "ties", "outlier", "inf", "zeros", "constant", "two_values", "tiny"])
+def test_segment_order_stats_select_edge_cases(rt, kind):
+    """The binned selection of segment_order_stats_kernel and its bitonic
+    fallback on the distributions that stress them: heavy ties (small
+    integers), a far outlier crowding the rest into one bin, +-inf values,
+    signed zeros, constant and two-valued segments, values rounded to two
+    decimals (ties inside the selected bins), and segments too short
+    to bin -- the requested ranks (numpy's 'linear' percentile ranks and the
+    extremes) equal numpy's sorted values."""
+    import ctypes
+    import torch
+    from riptide_amd import _lib
+    from riptide_amd.peaks import percentile_ranks
+    L_ = _lib.load()
+    rng = np.random.default_rng(7)
+    for per_seg in ((1, 2, 3, 5, 64, 65) if kind == "tiny" else (97, 4096, 5000, 20000)):
+        B, W, nseg = 2, 3, 2
+        L = nseg * per_seg + 3
+        if kind == "rounded":        # ties within the selected bins (binned path)
+            snr = np.round(rng.standard_normal((B, L, W)), 2).astype(np.float32)
+        elif kind == "ties":
+            snr = rng.integers(-3, 4, (B, L, W)).astype(np.float32)
+        elif kind == "outlier":
+            snr = rng.standard_normal((B, L, W)).astype(np.float32)
+            snr[:, ::max(per_seg // 3, 1), :] = 3.0e37
+            snr[0, 1, 0] = -2.5e38
+        elif kind == "inf":
+            snr = rng.standard_normal((B, L, W)).astype(np.float32)
+            snr[0, 2, :] = np.inf
+            snr[1, per_seg + 1, :] = -np.inf
+        elif kind == "zeros":
+            snr = np.where(rng.random((B, L, W)) < 0.5, np.float32(-0.0), np.float32(0.0))
+            snr[:, ::7, :] = rng.standard_normal((B, (L + 6) // 7, W))
+        elif kind == "constant":
+            snr = np.full((B, L, W), 4.25, dtype=np.float32)
+        elif kind == "two_values":
+            snr = np.where(rng.random((B, L, W)) < 0.3, np.float32(1.0), np.float32(1.0000001))
+        else:
+            snr = rng.standard_normal((B, L, W)).astype(np.float32)
+        snr = np.ascontiguousarray(snr, dtype=np.float32)
+        lohi, _ = percentile_ranks(per_seg)
+        ranks = np.concatenate([lohi, [0, per_seg - 1]]).astype(np.uint32)
+        d = torch.from_numpy(snr).cuda()
+        out = torch.empty((B, W, nseg, ranks.size), dtype=torch.float32, device="cuda")
+        rc = L_.rt_segment_order_stats_device(_lib.ptr(d), B, L * W, L, W, nseg, per_seg, _lib.ptr(ranks),
+                                              ranks.size, _lib.ptr(out),
+                                              ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        assert rc == 0, L_.rt_last_error()
+        got = out.cpu().numpy()
+        for b in range(B):
+            for iw in range(W):
+                for sg in range(nseg):
+                    col = snr[b, sg * per_seg:(sg + 1) * per_seg, iw]
+                    assert np.array_equal(got[b, iw, sg], np.sort(col)[ranks]), (kind, per_seg, b, iw, sg)
+
+
 def test_device_find_peaks_long_segments(rt):
     """find_peaks with segments of more than 4096 periods on the device path
     (a wide segwidth), identical to the host computation."""
