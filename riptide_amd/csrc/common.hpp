@@ -155,7 +155,7 @@ RT_HD inline int fill_chunks_bound(int n, int p, int runs) { return (n * p + 6 *
 RT_HD inline int pack_blob_words(int entries, int nb) { return (kBlobHeader + entries + nb + 2 * kMaxLevels + 4) & ~3; }
 
 // Merge variant for rows of p phase bins: slots per row rounded up to an
-// instantiated width (1..5, 8, 16, 45), or kPack2 for p <= 32 (short rows:
+// instantiated width (1..5, 8, 11, 16, 22, 45), or kPack2 for p <= 32 (short rows:
 // (row, 8-bin segment) tasks, ffa_kernels.hip merge_step_tasks); 0 if p is
 // too wide for the LDS engine.  The value is the cone kernel's template
 // argument and launch bucket.
@@ -167,7 +167,9 @@ RT_HD inline int merge_slots(uint32_t p)
     const int s = (int)((p + 63) / 64);
     if (s <= 5) return s;
     if (s <= 8) return 8;
+    if (s <= 11) return 11;
     if (s <= 16) return 16;
+    if (s <= 22) return 22;
     if (s <= kMaxSlots) return kMaxSlots;
     return 0;
 }

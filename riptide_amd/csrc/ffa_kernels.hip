@@ -2669,8 +2669,17 @@ __device__ __forceinline__ void snr_segments(const ConeArgs& a, const UnitView& 
 // Phase-bin range [lo, hi] a cone kernel variant runs, and the S/N lane-group
 // size G of a row of p bins: the epilogue instantiates only the row shapes its
 // variant can meet (smaller kernels; the rest is compiled out).
-constexpr int variant_pmin(int smax) { return smax == kPack2 ? 1 : (smax <= 5 ? 64 * (smax - 1) + 1 : (smax == 8 ? 321 : (smax == 16 ? 513 : 1025))); }
-constexpr int variant_pmax(int smax) { return smax == kPack2 ? 32 : (smax <= 5 ? 64 * smax : (smax == 8 ? 512 : (smax == 16 ? 1024 : 64 * kMaxSlots))); }
+// The wide variants' slot widths are the register staging's breakpoints
+// (merge_rows_per_wave = 45 / slots rows per wave): 11 slots stage 4 rows
+// per wave (32-row units at p = 513-704, where 16 slots staged 2), 22 slots
+// 2 (16-row units at p = 1025-1408, where 45 slots staged 1).
+constexpr int variant_pmin(int smax)
+{
+    return smax == kPack2 ? 1
+                          : (smax <= 5 ? 64 * (smax - 1) + 1
+                                       : (smax == 8 ? 321 : (smax == 11 ? 513 : (smax == 16 ? 705 : (smax == 22 ? 1025 : 1409)))));
+}
+constexpr int variant_pmax(int smax) { return smax == kPack2 ? 32 : 64 * smax; }
 constexpr bool variant_has_group(int smax, int G)
 {
     return snr_group(variant_pmin(smax)) <= G && G <= snr_group(variant_pmax(smax));
@@ -3117,7 +3126,9 @@ hipError_t launch_cone(const ConeArgs& args_in, uint32_t smax, uint32_t rw, bool
     case 4: e = launch_kind<4>(args, g, b, wide_snr, snr, s); break;
     case 5: e = launch_kind<5>(args, g, b, wide_snr, snr, s); break;
     case 8: e = launch_kind<8>(args, g, b, wide_snr, snr, s); break;
+    case 11: e = launch_kind<11>(args, g, b, wide_snr, snr, s); break;
     case 16: e = launch_kind<16>(args, g, b, wide_snr, snr, s); break;
+    case 22: e = launch_kind<22>(args, g, b, wide_snr, snr, s); break;
     case kMaxSlots: e = launch_kind<kMaxSlots>(args, g, b, wide_snr, snr, s); break;
     case kPack2: e = launch_kind<kPack2>(args, g, b, wide_snr, snr, s); break;
     default: return hipErrorInvalidValue;

@@ -58,7 +58,12 @@ def test_ffa2_golden_bit_exact(rt, golden, m, p, seed):
                                  (65537, 32),
                                  # 5-slot rows: through the roll table (257-260 bins: one and four
                                  # fifth-slot bins) and without it (261-320)
-                                 (3001, 257), (2999, 260), (4099, 261), (2000, 300), (1000, 320)])
+                                 (3001, 257), (2999, 260), (4099, 261), (2000, 300), (1000, 320),
+                                 # wide rows, every slot-width variant and its edges (8: 321-512,
+                                 # 11: 513-704, 16: 705-1024, 22: 1025-1408, 45: 1409-2880)
+                                 (3000, 512), (3001, 513), (2500, 520), (1999, 704), (1500, 705),
+                                 (1201, 1024), (1201, 1025), (1100, 1040), (900, 1408), (700, 1409),
+                                 (333, 2880)])
 def test_ffa2_vs_oracle(rt, oracle, m, p):
     x = np.random.RandomState(m * 31 + p).normal(size=(m, p)).astype(np.float32)
     assert np.array_equal(rt.ffa2(x), oracle.ffa2(x))
