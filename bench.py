@@ -283,7 +283,8 @@ def bench_cfg5(args, torch, dist, world, rank, local, dev):
             "config": {"workload": "cfg5: rffa search stage on SIGPROC .tim files (example.yaml ranges short / "
                                    "medium / long, smin 6), dispatch.search_files, DMIterator chunks of --batch "
                                    "files with the next chunk prefetched",
-                       "files_per_gpu": files, "chunk": args.batch, "peaks_found": cold[1],
+                       "files_per_gpu": files, "chunk": args.batch,
+                       "scratch_mfloats_per_buffer_trial": float(os.environ.get("RIPTIDE_AMD_SCRATCH_MFLOATS", "96")), "peaks_found": cold[1],
                        "clusters_found": cold[2], "clustering_radius_per_tobs": CFG5_CLUSTER_RADIUS,
                        "timed": "file read + H2D + deredden + normalise + 3 ranges' periodograms + device "
                                 "peak detection + gather + sort by period + cluster1d (pipeline.py:177-215)",
@@ -536,6 +537,12 @@ def main():
         if args.workload == "cfg3" and not user_cosched and not args.one_gpu_rehearsal:
             os.environ["RIPTIDE_AMD_COSCHED"] = "1"
         os.environ.setdefault("RIPTIDE_AMD_SCRATCH_MFLOATS", "1536" if big else "384")
+    if args.workload == "cfg5" and not user_scratch:
+        # cfg5's three range plans at 384 M floats per buffer and trial:
+        # fewer transform groups and cone launches than the 96 M default,
+        # 165.8 / 166.8 -> 185.4 DM trials/s (co-scheduling on top: 183.0;
+        # profiles/r06i6_ab_cfg5_scratch.log), within HBM at batch 16
+        os.environ["RIPTIDE_AMD_SCRATCH_MFLOATS"] = "384"
     import torch
     import torch.distributed as dist
     from riptide_amd import engine
